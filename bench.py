@@ -1,0 +1,210 @@
+#!/usr/bin/env python3
+"""Benchmark of the reference hot path: the vortex-merger SSP-RK3 step
+(19_NS2D_Vortex_Merger/vm.jl:12-90 + Common.jl:97-182) on MI355X through libcfdj.so.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+One "step" = one full RK3 step (3 RHS evaluations = 3 FFT Poisson solves + 3 fused
+Arakawa/Laplacian/RK stage kernels) over the whole grid, all data resident in HBM.
+N = 1 runs BASELINE.json config 3 (4096^2, re = 1000, dt = 5e-4: the reference's dt = .01
+is unstable at this size).  N > 1 is weak scaling on the y-slab ladder
+4096^2 -> 5760^2 -> 8192^2 -> 11520^2 (~16.7 M cells per GPU), RCCL halos + all-to-all.
+
+Rank 0 prints ONE JSON line (metric / value = whole-job MLUPS, roofline of the fused stage
+kernel from live HIP-event timing, cpu_baseline = the NumPy oracle on this host).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "MLUPS (cell-updates/s) + achieved HBM GB/s, 4096² vortex-merger RK3 step"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+# Algorithmic HBM bytes per cell: stage kernels 24 + 32 + 32 per step,
+# Poisson 32 per solve (D2Z read 8 + write ~8, Z2D read ~8 + write 8; divide fused).
+STAGE_BYTES_PER_CELL_STEP = 24 + 32 + 32
+STEP_BYTES_PER_CELL = 184
+WEAK_LADDER = {1: 4096, 2: 5760, 4: 8192, 8: 11520}
+
+
+def grid_for(n_gpus, nx_override=None):
+    if nx_override:
+        return nx_override
+    if n_gpus in WEAK_LADDER:
+        return WEAK_LADDER[n_gpus]
+    step = 128 * n_gpus // math.gcd(128, n_gpus)
+    return max(step, int(round(4096 * math.sqrt(n_gpus) / step)) * step)
+
+
+def stable_dt(nx):
+    # 5e-4 at 4096^2 (RK3 viscous limit 7.39e-4), scaled with dx^2
+    return 5e-4 * (4096.0 / nx) ** 2
+
+
+def cpu_baseline(nx, steps, workers):
+    """The CPU oracle (NumPy + scipy.fft restatement of vm.jl/Common.jl) on this host."""
+    from oracle import vm_oracle as vo
+
+    dx, dy, x, y = vo.vm_grid(nx, nx)
+    w = vo.vm_ic(nx, nx, x, y)
+    dt = stable_dt(nx)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        w = vo.rk3_step(w, dt, dx, dy, 1000.0, workers=workers)
+    t = time.perf_counter() - t0
+    return {"value": round(nx * nx * steps / t / 1e6, 4), "unit": "MLUPS", "cores": workers,
+            "kind": "port",
+            "sample": f"{steps} RK3 steps of the {nx}^2 vortex merger, NumPy oracle "
+                      f"(oracle/vm_oracle.py; scipy.fft workers={workers}, stencil single-"
+                      f"threaded NumPy), {t:.1f} s; Julia reference not runnable here"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--nx", type=int, default=None, help="override the grid size")
+    ap.add_argument("--rows-per-wave", type=int, default=None)
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true",
+                    help="do not record per-kernel HIP events in the timed region")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    n_gpus = max(world, 1)
+    if args.gpus != n_gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from cfd_julia_amd import VortexMerger, _lib
+    from cfd_julia_amd.common import vm_ic
+
+    _lib.require_gpu()
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        # host-side coordination only (unique-id broadcast, barriers, max-reduce);
+        # the data path (halos, FFT all-to-all) is RCCL inside libcfdj.so
+        dist.init_process_group("gloo")
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    nx = ny = grid_for(n_gpus, args.nx)
+    dx = dy = 2 * math.pi / nx
+    dt = stable_dt(nx)
+    re = 1000.0
+
+    if world > 1:
+        uid = VortexMerger.unique_id() if rank == 0 else bytes(128)
+        t = torch.frombuffer(bytearray(uid), dtype=torch.uint8)
+        dist.broadcast(t, src=0)
+        h = VortexMerger(nx, ny, dx, dy, re, device=local_rank, kind="dist", nranks=world,
+                         rank=rank, nccl_id=bytes(t.numpy().tobytes()))
+    else:
+        h = VortexMerger(nx, ny, dx, dy, re, device=local_rank)
+    if args.rows_per_wave:
+        h.set_rows_per_wave(args.rows_per_wave)
+
+    # vm.jl:107-128 IC on the global grid (every rank uploads its own slab of it)
+    x = dx * np.arange(nx + 1)
+    wn = np.empty((nx + 2, ny + 2), order="F")
+    vm_ic(nx, ny, x, x, wn)
+    wn[0, :] = wn[nx, :]
+    wn[:, 0] = wn[:, ny]
+    wn[nx + 1, :] = wn[1, :]
+    wn[:, ny + 1] = wn[:, 1]
+    h.upload(wn)
+    del wn
+
+    h.step(dt, args.warmup)
+    h.set_timing(not args.no_timing)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    h.step_async(dt, args.steps)
+    h.sync()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern = h.timing()
+    h.set_timing(False)
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt[0])
+
+    # sanity: the state stays finite and bounded (conservative scheme)
+    h.set_check_finite(True)
+    h.sync()
+
+    cells = nx * ny
+    value = cells * args.steps / elapsed / 1e6
+    ms_step = elapsed * 1e3 / max(args.steps, 1)
+    local_cells = cells / n_gpus
+    stage_ms, stage_n = kern["stage"]
+    stage_alg_bytes = STAGE_BYTES_PER_CELL_STEP * local_cells * args.steps
+    stage_gbs = stage_alg_bytes / (stage_ms * 1e-3) / 1e9 if stage_ms > 0 else None
+    roofline = {
+        "kernel": "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)",
+        "bound": "hbm",
+        "achieved": round(stage_gbs, 1) if stage_gbs else None,
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(stage_gbs / HBM_PEAK_GBS, 4) if stage_gbs else None,
+        "traffic": None,
+        "alg_bytes_per_launch": int(round(stage_alg_bytes / max(stage_n, 1))),
+        "avg_launch_us": round(stage_ms * 1e3 / max(stage_n, 1), 2),
+        "launches": stage_n,
+    }
+    step_gbs = STEP_BYTES_PER_CELL * local_cells * args.steps / elapsed / 1e9
+    breakdown = {k: {"ms_per_step": round(v[0] / max(args.steps, 1), 4), "launches": v[1]}
+                 for k, v in kern.items() if v[1]}
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "MLUPS",
+        "n_gpus": n_gpus,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: vm_ic two-Gaussian vortex-merger IC (Common.jl:208-219)",
+        "config": {"workload": f"NS2D vortex merger {nx}x{ny} periodic, Arakawa + FD-FFT "
+                               f"Poisson + SSP-RK3 (vm.jl)", "nx": nx, "ny": ny, "dt": dt,
+                   "re": re, "parallelism": "single" if n_gpus == 1 else f"yslab{n_gpus}"},
+        "achieved_hbm_gbs_step": round(step_gbs, 1),
+        "step_roofline_frac": round(step_gbs / HBM_PEAK_GBS, 4),
+        "kernels": breakdown,
+        "roofline": roofline,
+    }
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+        workers = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+                      or os.cpu_count() or 1)
+        line["cpu_baseline"] = cpu_baseline(nx, args.cpu_steps, workers)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    h.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,873 @@
+// libcfdj.so host side: handles, rocFFT plans, RCCL communicator, the RK3 step driver and
+// the extern "C" ABI declared in include/cfdj.h.
+//
+// Device data layout: every field is a dense nx-by-rows fp64 block, x
+// contiguous (the reference's column-major first index), pitch nx.  No ghost layers are
+// stored: the periodic wrap in x is modular indexing inside the stage kernel, the wrap /
+// halo in y is a pair of row pointers (on one GPU: the slab's own last / first row; on
+// y-slabs: receive buffers filled by RCCL or, for virtual ranks, by device copies).
+#include "cfdj_internal.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+
+namespace cfdj {
+
+static thread_local std::string g_err;
+void set_error(const std::string& msg) { g_err = msg; }
+
+template <class F>
+static int guard(F&& f) {
+  try {
+    f();
+    return CFDJ_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return CFDJ_ERR_HIP;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return CFDJ_ERR_STATE;
+  } catch (...) {
+    set_error("unknown C++ exception");
+    return CFDJ_ERR_STATE;
+  }
+}
+
+static void fft_setup() {
+  static std::once_flag once;
+  static rocfft_status st = rocfft_status_success;
+  std::call_once(once, [] { st = rocfft_setup(); });
+  CFDJ_FFT(st);
+}
+
+static void select_device(int device) {
+  if (device >= 0) CFDJ_HIP(hipSetDevice(device));
+}
+
+template <class T>
+static T* dalloc(size_t n) {
+  void* p = nullptr;
+  CFDJ_HIP(hipMalloc(&p, n * sizeof(T) + 16));
+  return static_cast<T*>(p);
+}
+
+template <class T>
+static void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+// Common.jl:106-113 wavenumber table (0-based): kx[0] = eps, kx[m] = hx*m for m < nx/2,
+// kx[m] = hx*(m - nx) for m >= nx/2, hx = 2pi/nx.
+static std::vector<double> kx_table(int nx, double eps) {
+  std::vector<double> kx(nx);
+  const double hx = (2.0 * M_PI) / nx;
+  const int h = nx / 2;
+  for (int i = 1; i <= h; ++i) {
+    kx[i - 1] = hx * (double)(i - 1);
+    kx[i + h - 1] = hx * (double)(i - h - 1);
+  }
+  kx[0] = eps;
+  return kx;
+}
+
+static void check_grid(int nx, int ny, double dx, double dy) {
+  CFDJ_REQUIRE(nx >= 4 && ny >= 4, "nx and ny must be >= 4");
+  CFDJ_REQUIRE(nx % 2 == 0, "nx must be even (Common.jl:108 loops to nx/2)");
+  CFDJ_REQUIRE(ny <= nx, "ny > nx: Common.jl:113 aliases ky = kx (BoundsError)");
+  CFDJ_REQUIRE(dx > 0 && dy > 0 && std::isfinite(dx) && std::isfinite(dy),
+               "dx, dy must be positive and finite");
+}
+
+// ---- spectral symbol tables + constants (Common.jl:101-103, 119-121) ----------------
+struct Symbol {
+  int nx = 0, ny = 0, nxh = 0;
+  double aa = 0, bb = 0, cc = 0, scale = 0;
+  double* cx = nullptr;  // cos(kx[m]), m < nxh
+  double* cy = nullptr;  // cos(ky[n]) = cos(kx[n]), n < ny
+  void init(int nx_, int ny_, double dx, double dy, double eps) {
+    nx = nx_;
+    ny = ny_;
+    nxh = nx / 2 + 1;
+    aa = -2.0 / (dx * dx) - 2.0 / (dy * dy);
+    bb = 2.0 / (dx * dx);
+    cc = 2.0 / (dy * dy);
+    scale = 1.0 / ((double)nx * (double)ny);  // ifft normalisation, folded into divide
+    std::vector<double> kx = kx_table(nx, eps), hcx(nxh), hcy(ny);
+    for (int m = 0; m < nxh; ++m) hcx[m] = std::cos(kx[m]);
+    for (int n = 0; n < ny; ++n) hcy[n] = std::cos(kx[n]);
+    cx = dalloc<double>(nxh);
+    cy = dalloc<double>(ny);
+    CFDJ_HIP(hipMemcpy(cx, hcx.data(), nxh * sizeof(double), hipMemcpyHostToDevice));
+    CFDJ_HIP(hipMemcpy(cy, hcy.data(), ny * sizeof(double), hipMemcpyHostToDevice));
+  }
+  void destroy() {
+    dfree(cx);
+    dfree(cy);
+  }
+  DivideParams divide(double2* spec, int width, int rows, int pitch, int kx_off,
+                      bool neg) const {
+    DivideParams p;
+    p.spec = spec;
+    p.cx = cx;
+    p.cy = cy;
+    p.width = width;
+    p.rows = rows;
+    p.pitch = pitch;
+    p.kx_off = kx_off;
+    p.nxh = nxh;
+    p.aa = aa;
+    p.bb = bb;
+    p.cc = cc;
+    p.scale = scale;
+    p.neg = neg;
+    return p;
+  }
+};
+
+// ---- rocFFT plan bundle --------------------------------------------------------------
+struct Plans {
+  std::vector<rocfft_plan> plans;
+  rocfft_execution_info info = nullptr;
+  void* work = nullptr;
+  size_t work_bytes = 0;
+
+  rocfft_plan add(rocfft_transform_type type, rocfft_result_placement place, size_t dim,
+                  const size_t* lengths, size_t batch, rocfft_plan_description desc) {
+    rocfft_plan p = nullptr;
+    CFDJ_FFT(rocfft_plan_create(&p, place, type, rocfft_precision_double, dim, lengths, batch,
+                                desc));
+    plans.push_back(p);
+    size_t wb = 0;
+    CFDJ_FFT(rocfft_plan_get_work_buffer_size(p, &wb));
+    if (wb > work_bytes) work_bytes = wb;
+    return p;
+  }
+  void finalize(hipStream_t st) {
+    CFDJ_FFT(rocfft_execution_info_create(&info));
+    CFDJ_FFT(rocfft_execution_info_set_stream(info, st));
+    if (work_bytes) {
+      CFDJ_HIP(hipMalloc(&work, work_bytes));
+      CFDJ_FFT(rocfft_execution_info_set_work_buffer(info, work, work_bytes));
+    }
+  }
+  void exec(rocfft_plan p, const void* in, void* out) {
+    void* ib[1] = {const_cast<void*>(in)};
+    void* ob[1] = {out};
+    CFDJ_FFT(rocfft_execute(p, ib, out ? ob : nullptr, info));
+  }
+  void destroy() {
+    for (auto p : plans) rocfft_plan_destroy(p);
+    plans.clear();
+    if (info) rocfft_execution_info_destroy(info);
+    info = nullptr;
+    if (work) (void)hipFree(work);
+    work = nullptr;
+  }
+};
+
+}  // namespace cfdj
+
+using namespace cfdj;
+
+// =====================================================================================
+// Poisson handle (Common.jl:97-125 / fft_p.jl:8-42)
+// =====================================================================================
+struct cfdj_fps_plan {
+  int device = -1;
+  hipStream_t stream = nullptr;
+  Symbol sym;
+  Plans plans;
+  rocfft_plan fwd = nullptr, inv = nullptr;
+  double2* spec = nullptr;
+  double *f_dev = nullptr, *s_dev = nullptr;
+
+  void solve_device(const double* f, double* s) {
+    plans.exec(fwd, f, spec);
+    launch_divide(sym.divide(spec, sym.nxh, sym.ny, sym.nxh, 0, false), stream);
+    plans.exec(inv, spec, s);
+  }
+  ~cfdj_fps_plan() {
+    plans.destroy();
+    sym.destroy();
+    dfree(spec);
+    dfree(f_dev);
+    dfree(s_dev);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// =====================================================================================
+// Vortex-merger handle (vm.jl:12-90 + Common.jl:132-182)
+// =====================================================================================
+namespace cfdj {
+
+enum class Mode { Single, Virtual, Rccl };
+
+struct Slab {
+  int rank = 0, row0 = 0, rows = 0;
+  double *wn = nullptr, *wa = nullptr, *wb = nullptr, *psi = nullptr;
+  double* ghost = nullptr;  // 4 rows: w_lo, w_hi, s_lo, s_hi (slab mode only)
+  double2 *X = nullptr, *S = nullptr, *Y = nullptr;  // slab-FFT buffers
+  void destroy() {
+    dfree(wn);
+    dfree(wa);
+    dfree(wb);
+    dfree(psi);
+    dfree(ghost);
+    dfree(X);
+    dfree(S);
+    dfree(Y);
+  }
+};
+
+}  // namespace cfdj
+
+struct cfdj_vm {
+  Mode mode = Mode::Single;
+  int nx = 0, ny = 0, nranks = 1, rank = 0, rows = 0, nxh = 0, kb = 0;
+  double dx = 0, dy = 0, re = 0, eps = 0;
+  int device = -1;
+  int rows_per_wave = 16;
+  hipStream_t stream = nullptr;
+  std::vector<Slab> slabs;
+  Symbol sym;
+  Plans plans;
+  rocfft_plan fwd2d = nullptr, inv2d = nullptr;                  // Single
+  rocfft_plan row_fwd = nullptr, row_inv = nullptr, col_fwd = nullptr, col_inv = nullptr;
+  double2* spec = nullptr;                                       // Single
+  ncclComm_t comm = nullptr;
+  double* gather = nullptr;                                      // Rccl download buffer
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev;
+  std::vector<int> ev_cat;
+  size_t ev_used = 0;
+  double ms[CFDJ_K_COUNT] = {};
+  long launches[CFDJ_K_COUNT] = {};
+  // finiteness check
+  bool check_finite = false;
+  int* d_flag = nullptr;
+
+  bool slab_mode() const { return mode != Mode::Single; }
+
+  // ---- timing -----------------------------------------------------------------------
+  void tbegin(int cat) {
+    if (!timing) return;
+    if (ev_used + 2 > ev.size()) {
+      for (int i = 0; i < 64; ++i) {
+        hipEvent_t e;
+        CFDJ_HIP(hipEventCreate(&e));
+        ev.push_back(e);
+      }
+    }
+    CFDJ_HIP(hipEventRecord(ev[ev_used], stream));
+    ev_cat.push_back(cat);
+  }
+  void tend() {
+    if (!timing) return;
+    CFDJ_HIP(hipEventRecord(ev[ev_used + 1], stream));
+    ev_used += 2;
+  }
+  void harvest() {  // after a stream sync
+    if (!timing) return;
+    for (size_t i = 0; i < ev_used / 2; ++i) {
+      float t = 0.f;
+      CFDJ_HIP(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
+      ms[ev_cat[i]] += t;
+      launches[ev_cat[i]] += 1;
+    }
+    ev_used = 0;
+    ev_cat.clear();
+  }
+
+  // ---- communication (slab mode) ------------------------------------------------------
+  // All-to-all of `count` complex elements per peer: send chunk q of slab p -> recv chunk
+  // p of slab q.  pick(slab, send?) selects the buffers.
+  template <class Pick>
+  void alltoall(Pick pick, size_t count) {
+    tbegin(CFDJ_K_COMM);
+    if (mode == Mode::Rccl) {
+      Slab& s = slabs[0];
+      CFDJ_NCCL(ncclAllToAll(pick(s, true), pick(s, false), 2 * count, ncclDouble, comm,
+                             stream));
+    } else {
+      const size_t bytes = count * sizeof(double2);
+      for (auto& sp : slabs)
+        for (auto& sq : slabs)
+          CFDJ_HIP(hipMemcpyAsync(pick(sq, false) + (size_t)sp.rank * count,
+                                  pick(sp, true) + (size_t)sq.rank * count, bytes,
+                                  hipMemcpyDeviceToDevice, stream));
+    }
+    tend();
+  }
+
+  // Fill the lo/hi ghost rows (offset 0/1 for w, 2/3 for psi) of every slab from the
+  // neighbouring slabs' last/first rows.
+  void halo(bool psi_field, const std::vector<const double*>& src) {
+    const int off = psi_field ? 2 : 0;
+    const size_t bytes = (size_t)nx * sizeof(double);
+    tbegin(CFDJ_K_COMM);
+    if (mode == Mode::Rccl) {
+      Slab& s = slabs[0];
+      const int prev = (rank + nranks - 1) % nranks, next = (rank + 1) % nranks;
+      const double* first = src[0];
+      const double* last = src[0] + (size_t)(rows - 1) * nx;
+      double* lo = s.ghost + (size_t)(off + 0) * nx;
+      double* hi = s.ghost + (size_t)(off + 1) * nx;
+      // Order matters when prev == next (2 ranks): sends [to prev, to next], receives
+      // [from next, from prev] so the k-th message between a pair matches by role.
+      CFDJ_NCCL(ncclGroupStart());
+      CFDJ_NCCL(ncclSend(first, nx, ncclDouble, prev, comm, stream));
+      CFDJ_NCCL(ncclSend(last, nx, ncclDouble, next, comm, stream));
+      CFDJ_NCCL(ncclRecv(hi, nx, ncclDouble, next, comm, stream));
+      CFDJ_NCCL(ncclRecv(lo, nx, ncclDouble, prev, comm, stream));
+      CFDJ_NCCL(ncclGroupEnd());
+    } else {
+      const int P = (int)slabs.size();
+      for (int p = 0; p < P; ++p) {
+        const int prev = (p + P - 1) % P, next = (p + 1) % P;
+        double* lo = slabs[p].ghost + (size_t)(off + 0) * nx;
+        double* hi = slabs[p].ghost + (size_t)(off + 1) * nx;
+        CFDJ_HIP(hipMemcpyAsync(lo, src[prev] + (size_t)(slabs[prev].rows - 1) * nx, bytes,
+                                hipMemcpyDeviceToDevice, stream));
+        CFDJ_HIP(hipMemcpyAsync(hi, src[next], bytes, hipMemcpyDeviceToDevice, stream));
+      }
+    }
+    tend();
+  }
+
+  // ---- Poisson: psi = fps(-w)  (Common.jl:134-136) ------------------------------------
+  void poisson(const std::vector<const double*>& src, bool neg) {
+    if (!slab_mode()) {
+      Slab& s = slabs[0];
+      tbegin(CFDJ_K_FFT_FWD);
+      plans.exec(fwd2d, src[0], spec);
+      tend();
+      tbegin(CFDJ_K_DIVIDE);
+      launch_divide(sym.divide(spec, nxh, ny, nxh, 0, neg), stream);
+      tend();
+      tbegin(CFDJ_K_FFT_INV);
+      plans.exec(inv2d, spec, s.psi);
+      tend();
+      return;
+    }
+    const size_t cnt = (size_t)rows * kb;
+    for (size_t i = 0; i < slabs.size(); ++i) {
+      Slab& s = slabs[i];
+      tbegin(CFDJ_K_FFT_FWD);
+      plans.exec(row_fwd, src[i], s.X);
+      tend();
+      tbegin(CFDJ_K_COMM);
+      launch_pack(s.X, s.S, nxh, rows, kb, nranks, stream);
+      tend();
+    }
+    alltoall([](Slab& s, bool send) { return send ? s.S : s.Y; }, cnt);
+    for (auto& s : slabs) {
+      tbegin(CFDJ_K_FFT_FWD);
+      plans.exec(col_fwd, s.Y, nullptr);
+      tend();
+      tbegin(CFDJ_K_DIVIDE);
+      launch_divide(sym.divide(s.Y, kb, ny, kb, s.rank * kb, neg), stream);
+      tend();
+      tbegin(CFDJ_K_FFT_INV);
+      plans.exec(col_inv, s.Y, nullptr);
+      tend();
+    }
+    alltoall([](Slab& s, bool send) { return send ? s.Y : s.S; }, cnt);
+    for (size_t i = 0; i < slabs.size(); ++i) {
+      Slab& s = slabs[i];
+      tbegin(CFDJ_K_COMM);
+      launch_unpack(s.S, s.X, nxh, rows, kb, nranks, stream);
+      tend();
+      tbegin(CFDJ_K_FFT_INV);
+      plans.exec(row_inv, s.X, s.psi);
+      tend();
+    }
+  }
+
+  StageParams stage_params(const Slab& s, const double* w, const double* wn, double* out,
+                           double dt) const {
+    StageParams p;
+    p.w = w;
+    p.s = s.psi;
+    if (slab_mode()) {
+      p.w_lo = s.ghost;
+      p.w_hi = s.ghost + nx;
+      p.s_lo = s.ghost + 2 * (size_t)nx;
+      p.s_hi = s.ghost + 3 * (size_t)nx;
+    } else {
+      p.w_lo = w + (size_t)(rows - 1) * nx;
+      p.w_hi = w;
+      p.s_lo = s.psi + (size_t)(rows - 1) * nx;
+      p.s_hi = s.psi;
+    }
+    p.wn = wn;
+    p.out = out;
+    p.nx = nx;
+    p.ny = rows;
+    p.rows_per_wave = rows_per_wave;
+    const double dx2 = dx * dx, dy2 = dy * dy;
+    p.k.aa = 1.0 / (re * dx2);
+    p.k.bb = 1.0 / (re * dy2);
+    p.k.gg = 1.0 / ((4.0 * dx) * dy);
+    p.k.hh = 1.0 / 3.0;
+    p.k.dt = dt;
+    p.k.c25dt = 0.25 * dt;
+    p.k.c23 = 2.0 / 3.0;
+    p.k.c23dt = (2.0 / 3.0) * dt;
+    return p;
+  }
+
+  // One RHS evaluation on the stage input + the fused stage update.
+  // stage 1: wn -> wa;  stage 2: (wa, wn) -> wb;  stage 3: (wb, wn) -> wn;  0: w -> out = r
+  void stage(int st, double dt) {
+    std::vector<const double*> src(slabs.size());
+    for (size_t i = 0; i < slabs.size(); ++i)
+      src[i] = st == 1 ? slabs[i].wn : st == 2 ? slabs[i].wa : slabs[i].wb;
+    poisson(src, true);
+    if (slab_mode()) {
+      halo(false, src);
+      std::vector<const double*> ps(slabs.size());
+      for (size_t i = 0; i < slabs.size(); ++i) ps[i] = slabs[i].psi;
+      halo(true, ps);
+    }
+    for (size_t i = 0; i < slabs.size(); ++i) {
+      Slab& s = slabs[i];
+      double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
+      tbegin(CFDJ_K_STAGE);
+      launch_stage(st, stage_params(s, src[i], s.wn, out, dt), stream);
+      tend();
+    }
+  }
+
+  void step_async(double dt, int nsteps) {
+    for (int n = 0; n < nsteps; ++n) {
+      stage(1, dt);
+      stage(2, dt);
+      stage(3, dt);
+    }
+  }
+
+  void sync() {
+    CFDJ_HIP(hipStreamSynchronize(stream));
+    harvest();
+    if (check_finite) {
+      CFDJ_HIP(hipMemsetAsync(d_flag, 0, sizeof(int), stream));
+      for (auto& s : slabs) launch_check_finite(s.wn, (size_t)nx * s.rows, d_flag, stream);
+      int flag = 0;
+      CFDJ_HIP(hipMemcpyAsync(&flag, d_flag, sizeof(int), hipMemcpyDeviceToHost, stream));
+      CFDJ_HIP(hipStreamSynchronize(stream));
+      if (flag) throw Error{CFDJ_ERR_NONFINITE, "non-finite vorticity after step"};
+    }
+  }
+
+  void init_buffers() {
+    nxh = nx / 2 + 1;
+    const int P = nranks;
+    kb = (nxh + P - 1) / P;
+    rows = ny / P;
+    const size_t n = (size_t)nx * rows;
+    for (auto& s : slabs) {
+      s.rows = rows;
+      s.row0 = s.rank * rows;
+      s.wn = dalloc<double>(n);
+      s.wa = dalloc<double>(n);
+      s.wb = dalloc<double>(n);
+      s.psi = dalloc<double>(n);
+      if (slab_mode()) {
+        s.ghost = dalloc<double>(4 * (size_t)nx);
+        s.X = dalloc<double2>((size_t)nxh * rows);
+        s.S = dalloc<double2>((size_t)P * kb * rows);
+        s.Y = dalloc<double2>((size_t)ny * kb);
+      }
+    }
+    if (slab_mode()) {
+      size_t len_x = (size_t)nx, len_y = (size_t)ny;
+      row_fwd = plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace, 1,
+                          &len_x, rows, nullptr);
+      row_inv = plans.add(rocfft_transform_type_real_inverse, rocfft_placement_notinplace, 1,
+                          &len_x, rows, nullptr);
+      rocfft_plan_description desc = nullptr;
+      CFDJ_FFT(rocfft_plan_description_create(&desc));
+      size_t stride = (size_t)kb;
+      CFDJ_FFT(rocfft_plan_description_set_data_layout(
+          desc, rocfft_array_type_complex_interleaved, rocfft_array_type_complex_interleaved,
+          nullptr, nullptr, 1, &stride, 1, 1, &stride, 1));
+      col_fwd = plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 1,
+                          &len_y, kb, desc);
+      col_inv = plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 1,
+                          &len_y, kb, desc);
+      rocfft_plan_description_destroy(desc);
+    } else {
+      size_t lens[2] = {(size_t)nx, (size_t)ny};
+      fwd2d = plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace, 2,
+                        lens, 1, nullptr);
+      inv2d = plans.add(rocfft_transform_type_real_inverse, rocfft_placement_notinplace, 2,
+                        lens, 1, nullptr);
+      spec = dalloc<double2>((size_t)nxh * ny);
+    }
+    plans.finalize(stream);
+    d_flag = dalloc<int>(1);
+  }
+
+  ~cfdj_vm() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto& s : slabs) s.destroy();
+    plans.destroy();
+    sym.destroy();
+    dfree(spec);
+    dfree(gather);
+    dfree(d_flag);
+    for (auto e : ev) (void)hipEventDestroy(e);
+    if (comm) ncclCommDestroy(comm);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+namespace {
+
+cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int device,
+                Mode mode, int nranks, int rank) {
+  check_grid(nx, ny, dx, dy);
+  CFDJ_REQUIRE(std::isfinite(re) && re != 0.0, "re must be finite and non-zero");
+  CFDJ_REQUIRE(nranks >= 1 && ny % nranks == 0, "ny must be divisible by the rank count");
+  CFDJ_REQUIRE(ny / nranks >= 2, "each slab needs at least 2 rows");
+  CFDJ_REQUIRE(rank >= 0 && rank < nranks, "rank out of range");
+  fft_setup();
+  select_device(device);
+  std::unique_ptr<cfdj_vm> h(new cfdj_vm);
+  CFDJ_HIP(hipGetDevice(&h->device));
+  h->mode = mode;
+  h->nx = nx;
+  h->ny = ny;
+  h->dx = dx;
+  h->dy = dy;
+  h->re = re;
+  h->eps = eps;
+  h->nranks = nranks;
+  h->rank = rank;
+  // rows per wavefront: keep >= ~8 waves per CU at the benchmark sizes
+  h->rows_per_wave = ny / nranks >= 2048 ? 16 : 8;
+  CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+  if (mode == Mode::Virtual) {
+    h->slabs.resize(nranks);
+    for (int p = 0; p < nranks; ++p) h->slabs[p].rank = p;
+  } else {
+    h->slabs.resize(1);
+    h->slabs[0].rank = rank;
+  }
+  h->sym.init(nx, ny, dx, dy, eps);
+  h->init_buffers();
+  return h.release();
+}
+
+void check_ld(long ld, long need, const char* what) {
+  if (ld < need) throw Error{CFDJ_ERR_ARG, std::string(what) + ": leading dimension too small"};
+}
+
+// Reference ghost fill of a ghosted (nx+2)x(ny+2) column-major array, vm.jl:68-76 /
+// Common.jl:138-146 order: row nx+2 <- 2, col ny+2 <- 2, row 1 <- nx+1, col 1 <- ny+1.
+void ghost_fill(double* g, long ld, int nx, int ny) {
+  auto at = [&](int i, int j) -> double& { return g[(size_t)(i - 1) + (size_t)(j - 1) * ld]; };
+  for (int j = 1; j <= ny + 2; ++j) at(nx + 2, j) = at(2, j);
+  for (int i = 1; i <= nx + 2; ++i) at(i, ny + 2) = at(i, 2);
+  for (int j = 1; j <= ny + 2; ++j) at(1, j) = at(nx + 1, j);
+  for (int i = 1; i <= nx + 2; ++i) at(i, 1) = at(i, ny + 1);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* cfdj_last_error(void) { return g_err.c_str(); }
+
+const char* cfdj_version(void) { return "cfdj 0.1.0 (gfx950)"; }
+
+int cfdj_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// ---- Poisson ---------------------------------------------------------------------------
+int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device,
+                    cfdj_fps_plan** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr, "out is NULL");
+    *out = nullptr;
+    check_grid(nx, ny, dx, dy);
+    fft_setup();
+    select_device(device);
+    std::unique_ptr<cfdj_fps_plan> h(new cfdj_fps_plan);
+    CFDJ_HIP(hipGetDevice(&h->device));
+    CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->sym.init(nx, ny, dx, dy, eps);
+    size_t lens[2] = {(size_t)nx, (size_t)ny};
+    h->fwd = h->plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace, 2,
+                          lens, 1, nullptr);
+    h->inv = h->plans.add(rocfft_transform_type_real_inverse, rocfft_placement_notinplace, 2,
+                          lens, 1, nullptr);
+    h->plans.finalize(h->stream);
+    h->spec = dalloc<double2>((size_t)h->sym.nxh * ny);
+    h->f_dev = dalloc<double>((size_t)nx * ny);
+    h->s_dev = dalloc<double>((size_t)nx * ny);
+    *out = h.release();
+  });
+}
+
+int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long lds) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && f && s, "NULL argument");
+    const int nx = h->sym.nx, ny = h->sym.ny;
+    check_ld(ldf, nx, "ldf");
+    check_ld(lds, nx, "lds");
+    select_device(h->device);
+    CFDJ_HIP(hipMemcpy2DAsync(h->f_dev, nx * sizeof(double), f, ldf * sizeof(double),
+                              nx * sizeof(double), ny, hipMemcpyHostToDevice, h->stream));
+    h->solve_device(h->f_dev, h->s_dev);
+    CFDJ_HIP(hipMemcpy2DAsync(s, lds * sizeof(double), h->s_dev, nx * sizeof(double),
+                              nx * sizeof(double), ny, hipMemcpyDeviceToHost, h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && f_dev && s_dev, "NULL argument");
+    select_device(h->device);
+    h->solve_device(f_dev, s_dev);
+  });
+}
+
+void cfdj_fps_destroy(cfdj_fps_plan* h) {
+  if (!h) return;
+  (void)guard([&] {
+    select_device(h->device);
+    delete h;
+  });
+}
+
+int cfdj_fps(int nx, int ny, double dx, double dy, double eps, const double* f, long ldf,
+             double* s, long lds) {
+  cfdj_fps_plan* h = nullptr;
+  int rc = cfdj_fps_create(nx, ny, dx, dy, eps, -1, &h);
+  if (rc != CFDJ_OK) return rc;
+  rc = cfdj_fps_solve(h, f, ldf, s, lds);
+  cfdj_fps_destroy(h);
+  return rc;
+}
+
+// ---- vortex merger -------------------------------------------------------------------
+int cfdj_vm_create(int nx, int ny, double dx, double dy, double re, double eps, int device,
+                   cfdj_vm** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr, "out is NULL");
+    *out = nullptr;
+    *out = new_vm(nx, ny, dx, dy, re, eps, device, Mode::Single, 1, 0);
+  });
+}
+
+int cfdj_vm_create_virtual(int nx, int ny, double dx, double dy, double re, double eps,
+                           int device, int nranks, cfdj_vm** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr, "out is NULL");
+    *out = nullptr;
+    *out = new_vm(nx, ny, dx, dy, re, eps, device, Mode::Virtual, nranks, 0);
+  });
+}
+
+int cfdj_comm_unique_id(void* out128) {
+  return guard([&] {
+    CFDJ_REQUIRE(out128 != nullptr, "out is NULL");
+    ncclUniqueId id;
+    CFDJ_NCCL(ncclGetUniqueId(&id));
+    std::memcpy(out128, &id, sizeof(id));
+  });
+}
+
+int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double eps,
+                        int device, int rank, int nranks, const void* nccl_id,
+                        cfdj_vm** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr && nccl_id != nullptr, "NULL argument");
+    *out = nullptr;
+    if (nranks == 1) {
+      *out = new_vm(nx, ny, dx, dy, re, eps, device, Mode::Single, 1, 0);
+      return;
+    }
+    std::unique_ptr<cfdj_vm> h(new_vm(nx, ny, dx, dy, re, eps, device, Mode::Rccl, nranks,
+                                      rank));
+    ncclUniqueId id;
+    std::memcpy(&id, nccl_id, sizeof(id));
+    CFDJ_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
+    *out = h.release();
+  });
+}
+
+int cfdj_vm_upload(cfdj_vm* h, const double* w, long ldw) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && w, "NULL argument");
+    check_ld(ldw, (long)h->nx + 2, "ldw");
+    select_device(h->device);
+    const int nx = h->nx;
+    for (auto& s : h->slabs) {
+      const double* src = w + 1 + (size_t)(1 + s.row0) * ldw;  // &w[2, 2 + row0]
+      CFDJ_HIP(hipMemcpy2DAsync(s.wn, nx * sizeof(double), src, ldw * sizeof(double),
+                                nx * sizeof(double), s.rows, hipMemcpyHostToDevice,
+                                h->stream));
+    }
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_vm_download(cfdj_vm* h, double* w, long ldw) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && w, "NULL argument");
+    check_ld(ldw, (long)h->nx + 2, "ldw");
+    select_device(h->device);
+    const int nx = h->nx;
+    double* dst = w + 1 + ldw;  // &w[2,2]
+    if (h->mode == Mode::Rccl) {
+      if (!h->gather) h->gather = dalloc<double>((size_t)nx * h->ny);
+      CFDJ_NCCL(ncclAllGather(h->slabs[0].wn, h->gather, (size_t)nx * h->rows, ncclDouble,
+                              h->comm, h->stream));
+      CFDJ_HIP(hipMemcpy2DAsync(dst, ldw * sizeof(double), h->gather, nx * sizeof(double),
+                                nx * sizeof(double), h->ny, hipMemcpyDeviceToHost,
+                                h->stream));
+    } else {
+      for (auto& s : h->slabs)
+        CFDJ_HIP(hipMemcpy2DAsync(dst + (size_t)s.row0 * ldw, ldw * sizeof(double), s.wn,
+                                  nx * sizeof(double), nx * sizeof(double), s.rows,
+                                  hipMemcpyDeviceToHost, h->stream));
+    }
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    ghost_fill(w, ldw, nx, h->ny);
+  });
+}
+
+int cfdj_vm_step_async(cfdj_vm* h, double dt, int nsteps) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(nsteps >= 0, "nsteps must be >= 0");
+    CFDJ_REQUIRE(std::isfinite(dt), "dt must be finite");
+    select_device(h->device);
+    h->step_async(dt, nsteps);
+  });
+}
+
+int cfdj_vm_sync(cfdj_vm* h) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    select_device(h->device);
+    h->sync();
+  });
+}
+
+int cfdj_vm_step(cfdj_vm* h, double dt, int nsteps) {
+  int rc = cfdj_vm_step_async(h, dt, nsteps);
+  if (rc != CFDJ_OK) return rc;
+  return cfdj_vm_sync(h);
+}
+
+int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, double* s,
+                long lds) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && w && r && s, "NULL argument");
+    CFDJ_REQUIRE(h->mode == Mode::Single, "cfdj_vm_rhs needs a single-GPU handle");
+    check_ld(ldw, (long)h->nx + 2, "ldw");
+    check_ld(ldr, (long)h->nx + 2, "ldr");
+    check_ld(lds, (long)h->nx + 2, "lds");
+    select_device(h->device);
+    const int nx = h->nx, ny = h->ny;
+    Slab& sl = h->slabs[0];
+    CFDJ_HIP(hipMemcpy2DAsync(sl.wa, nx * sizeof(double), w + 1 + ldw, ldw * sizeof(double),
+                              nx * sizeof(double), ny, hipMemcpyHostToDevice, h->stream));
+    h->poisson({sl.wa}, true);
+    h->tbegin(CFDJ_K_STAGE);
+    launch_stage(0, h->stage_params(sl, sl.wa, sl.wa, sl.wb, 0.0), h->stream);
+    h->tend();
+    CFDJ_HIP(hipMemcpy2DAsync(r + 1 + ldr, ldr * sizeof(double), sl.wb, nx * sizeof(double),
+                              nx * sizeof(double), ny, hipMemcpyDeviceToHost, h->stream));
+    CFDJ_HIP(hipMemcpy2DAsync(s + 1 + lds, lds * sizeof(double), sl.psi, nx * sizeof(double),
+                              nx * sizeof(double), ny, hipMemcpyDeviceToHost, h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    h->harvest();
+    ghost_fill(s, lds, nx, ny);
+  });
+}
+
+int cfdj_vm_set_timing(cfdj_vm* h, int enable) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    select_device(h->device);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    h->harvest();
+    h->timing = enable != 0;
+    for (int k = 0; k < CFDJ_K_COUNT; ++k) {
+      h->ms[k] = 0.0;
+      h->launches[k] = 0;
+    }
+  });
+}
+
+int cfdj_vm_timing(cfdj_vm* h, double* ms, long* launches) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    for (int k = 0; k < CFDJ_K_COUNT; ++k) {
+      if (ms) ms[k] = h->ms[k];
+      if (launches) launches[k] = h->launches[k];
+    }
+  });
+}
+
+int cfdj_vm_set_check_finite(cfdj_vm* h, int enable) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    h->check_finite = enable != 0;
+  });
+}
+
+int cfdj_vm_field_device(cfdj_vm* h, double** w_dev) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && w_dev, "NULL argument");
+    CFDJ_REQUIRE(h->mode != Mode::Virtual, "virtual-rank handles hold several slabs");
+    *w_dev = h->slabs[0].wn;
+  });
+}
+
+int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    if (row0) *row0 = h->mode == Mode::Virtual ? 0 : h->slabs[0].row0;
+    if (rows) *rows = h->mode == Mode::Virtual ? h->ny : h->rows;
+  });
+}
+
+int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(rows >= 1, "rows must be >= 1");
+    h->rows_per_wave = rows;
+  });
+}
+
+void cfdj_vm_destroy(cfdj_vm* h) {
+  if (!h) return;
+  (void)guard([&] {
+    select_device(h->device);
+    delete h;
+  });
+}
+
+}  // extern "C"

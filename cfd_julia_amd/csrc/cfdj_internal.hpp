@@ -1,0 +1,103 @@
+// Internal declarations shared by the libcfdj.so translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rocfft/rocfft.h>
+#include <rccl/rccl.h>
+
+#include <cstddef>
+#include <string>
+#include <vector>
+
+#include "cfdj.h"
+
+namespace cfdj {
+
+// ---- errors ------------------------------------------------------------------------
+void set_error(const std::string& msg);
+
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define CFDJ_HIP(expr)                                                                  \
+  do {                                                                                  \
+    hipError_t e_ = (expr);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      throw ::cfdj::Error{CFDJ_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)}; \
+  } while (0)
+
+#define CFDJ_FFT(expr)                                                                  \
+  do {                                                                                  \
+    rocfft_status s_ = (expr);                                                          \
+    if (s_ != rocfft_status_success)                                                    \
+      throw ::cfdj::Error{CFDJ_ERR_ROCFFT, std::string(#expr) + ": rocfft status " +     \
+                                               std::to_string((int)s_)};                \
+  } while (0)
+
+#define CFDJ_NCCL(expr)                                                                 \
+  do {                                                                                  \
+    ncclResult_t r_ = (expr);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      throw ::cfdj::Error{CFDJ_ERR_RCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)}; \
+  } while (0)
+
+#define CFDJ_REQUIRE(cond, msg)                                                         \
+  do {                                                                                  \
+    if (!(cond)) throw ::cfdj::Error{CFDJ_ERR_ARG, (msg)};                              \
+  } while (0)
+
+// ---- kernel parameter blocks --------------------------------------------------------
+// Constants of Common.jl:149-152 plus the RK3 stage weights of vm.jl:28,43-47,62-66.
+struct StageCoef {
+  double aa, bb, gg, hh;  // 1/(re dx^2), 1/(re dy^2), 1/(4dx dy), 1/3
+  double dt;              // stage 1: wn + dt*r
+  double c25dt;           // stage 2: (.75wn + .25wt) + (.25dt)*r
+  double c23, c23dt;      // stage 3: (wn/3 + (2/3)wt) + ((2/3)dt)*r
+};
+
+// One slab of rows [0, ny) (local), pitch nx, x contiguous.  Row -1 / row ny are read
+// from the lo / hi ghost rows (on one GPU: the periodic wrap rows of the same array).
+struct StageParams {
+  const double* w;     // stencil input omega_s
+  const double* w_lo;
+  const double* w_hi;
+  const double* s;     // streamfunction psi
+  const double* s_lo;
+  const double* s_hi;
+  const double* wn;    // omega^n (pointwise; stages 2 and 3)
+  double* out;         // stage output (stage 0: the bare RHS r)
+  int nx, ny;
+  int rows_per_wave;
+  StageCoef k;
+};
+
+void launch_stage(int stage, const StageParams& p, hipStream_t st);
+
+// Spectral divide (Common.jl:118-121) on a (width x rows) block of the half spectrum
+// stored with row pitch `pitch` (complex elements); column i of the block is the
+// global x-wavenumber index kx_off + i, row j the global y index.  Elements with global
+// kx >= nxh are padding and are zeroed.  neg folds the f = -w of Common.jl:134.
+struct DivideParams {
+  double2* spec;
+  const double* cx;  // cos(kx[m]), m = 0..nxh-1
+  const double* cy;  // cos(ky[n]), n = 0..ny-1
+  int width, rows, pitch, kx_off, nxh;
+  double aa, bb, cc, scale;
+  bool neg;
+};
+void launch_divide(const DivideParams& p, hipStream_t st);
+
+// Slab-FFT transposition helpers (multi-GPU / virtual ranks).
+// pack:   X[jl*nxh + kx] -> S[(q*rows + jl)*kb + kl],  kx = q*kb + kl (zero padding)
+// unpack: S[(q*rows + jl)*kb + kl] -> X[jl*nxh + kx]   (kx < nxh)
+void launch_pack(const double2* X, double2* S, int nxh, int rows, int kb, int nranks,
+                 hipStream_t st);
+void launch_unpack(const double2* S, double2* X, int nxh, int rows, int kb, int nranks,
+                   hipStream_t st);
+
+// Finiteness check: sets *flag = 1 if any element is not finite.
+void launch_check_finite(const double* a, size_t n, int* flag, hipStream_t st);
+
+}  // namespace cfdj

@@ -1,0 +1,243 @@
+// gfx950 kernels of the periodic vortex-merger step.
+//
+//  * vm_stage_kernel  -- fused Arakawa Jacobian + 5-point Laplacian (Common.jl:148-181)
+//                        + SSP-RK3 stage update (vm.jl:28, 43-47, 62-66).
+//  * divide_kernel    -- FD-symbol spectral divide of the FFT Poisson solve
+//                        (Common.jl:115-121).
+//  * pack / unpack    -- half-spectrum transposition blocks of the y-slab FFT.
+//
+// Built with -ffp-contract=off: every expression is evaluated in the order the reference
+// writes it (no FMA contraction), so given the same streamfunction the stencil output is
+// bit-identical to the CPU oracle (oracle/vm_oracle.py: arakawa_rhs, rk3_step).
+#include "cfdj_internal.hpp"
+
+namespace cfdj {
+
+namespace {
+
+constexpr int kWave = 64;
+constexpr int kWavesPerBlock = 4;
+constexpr int kColsPerWave = 2 * kWave;  // two x-adjacent points per lane (16-B loads)
+
+// Three values of one row around the lane's point pair: l = x-1, a = x, b = x+1, r = x+2.
+struct Win {
+  double l, a, b, r;
+};
+struct Raw {
+  double2 c;
+  double el, er;
+};
+
+__device__ __forceinline__ const double* row_ptr(const double* a, const double* lo,
+                                                 const double* hi, int y, int ny, int nx) {
+  return y < 0 ? lo : (y >= ny ? hi : a + (size_t)y * nx);
+}
+
+__device__ __forceinline__ Raw fetch(const double* row, int xs, int xl, int xr, bool is_l,
+                                     bool is_r) {
+  Raw r;
+  r.c = *reinterpret_cast<const double2*>(row + xs);
+  r.el = 0.0;
+  r.er = 0.0;
+  if (is_l) r.el = row[xl];
+  if (is_r) r.er = row[xr];
+  return r;
+}
+
+__device__ __forceinline__ Win expand(const Raw& raw, bool is_l, bool is_r) {
+  Win w;
+  w.a = raw.c.x;
+  w.b = raw.c.y;
+  const double up = __shfl_up(raw.c.y, 1, kWave);    // lane-1's x+1 == my x-1
+  const double dn = __shfl_down(raw.c.x, 1, kWave);  // lane+1's x   == my x+2
+  w.l = is_l ? raw.el : up;
+  w.r = is_r ? raw.er : dn;
+  return w;
+}
+
+// r = -J(w, s) + (1/re) lap(w) at one point; the argument names are compass directions
+// (E = i+1, N = j+1).  Float order of Common.jl:155-180.
+__device__ __forceinline__ double arakawa_rhs(double wc, double wE, double wW, double wN,
+                                              double wS, double wNE, double wSW, double wNW,
+                                              double wSE, double sE, double sW, double sN,
+                                              double sS, double sNE, double sSW,
+                                              double sNW, double sSE, const StageCoef& k) {
+  const double j1 = (wE - wW) * (sN - sS) - (wN - wS) * (sE - sW);
+  const double j2 =
+      wE * (sNE - sSE) - wW * (sNW - sSW) - wN * (sNE - sNW) + wS * (sSE - sSW);
+  const double j3 =
+      wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS);
+  const double jac = k.gg * (j1 + j2 + j3) * k.hh;
+  return -jac + (k.aa * (wE - 2.0 * wc + wW) + k.bb * (wN - 2.0 * wc + wS));
+}
+
+template <int STAGE>
+__device__ __forceinline__ double stage_update(double r, double wc, double wn,
+                                               const StageCoef& k) {
+  if constexpr (STAGE == 0) {
+    return r;
+  } else if constexpr (STAGE == 1) {
+    return wc + k.dt * r;  // vm.jl:28 (wc is wn here)
+  } else if constexpr (STAGE == 2) {
+    return (0.75 * wn + 0.25 * wc) + k.c25dt * r;  // vm.jl:43-47
+  } else {
+    return (wn / 3.0 + k.c23 * wc) + k.c23dt * r;  // vm.jl:62-66
+  }
+}
+
+// One wavefront owns 128 consecutive x (two per lane, 16-B loads) and marches
+// `rows_per_wave` rows in y with a 3-row register window of omega and psi; x-neighbours
+// come from lane shuffles, the two wave-edge values from one masked load each.  Four
+// independent wavefronts per 256-thread workgroup take four consecutive row chunks.
+template <int STAGE>
+__global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nx = p.nx, ny = p.ny;
+  const int x = blockIdx.x * kColsPerWave + 2 * lane;
+  const bool valid = x < nx;
+  const int xs = valid ? x : 0;
+  const bool is_l = lane == 0;
+  const bool is_r = (lane == kWave - 1) || (xs + 2 >= nx);
+  const int xl = xs == 0 ? nx - 1 : xs - 1;
+  const int xr = xs + 2 >= nx ? xs + 2 - nx : xs + 2;
+
+  const int ybeg = (blockIdx.y * kWavesPerBlock + wave) * p.rows_per_wave;
+  if (ybeg >= ny) return;
+  const int yend = min(ybeg + p.rows_per_wave, ny);
+
+  const StageCoef k = p.k;
+  Raw wr_p = fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg + 1, ny, nx), xs, xl, xr, is_l, is_r);
+  Raw sr_p = fetch(row_ptr(p.s, p.s_lo, p.s_hi, ybeg + 1, ny, nx), xs, xl, xr, is_l, is_r);
+  Win wm = expand(fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg - 1, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
+  Win sm = expand(fetch(row_ptr(p.s, p.s_lo, p.s_hi, ybeg - 1, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
+  Win wc = expand(fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
+  Win sc = expand(fetch(row_ptr(p.s, p.s_lo, p.s_hi, ybeg, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
+
+  for (int y = ybeg; y < yend; ++y) {
+    // prefetch row y+2 (clamped: the last iteration re-reads row yend, harmlessly)
+    const int yn = min(y + 2, yend);
+    const Raw wr_n = fetch(row_ptr(p.w, p.w_lo, p.w_hi, yn, ny, nx), xs, xl, xr, is_l, is_r);
+    const Raw sr_n = fetch(row_ptr(p.s, p.s_lo, p.s_hi, yn, ny, nx), xs, xl, xr, is_l, is_r);
+    double2 wnv = make_double2(0.0, 0.0);
+    if constexpr (STAGE >= 2) wnv = *reinterpret_cast<const double2*>(p.wn + (size_t)y * nx + xs);
+
+    const Win wp = expand(wr_p, is_l, is_r);
+    const Win sp = expand(sr_p, is_l, is_r);
+
+    // point x  : W = l, C = a, E = b      point x+1: W = a, C = b, E = r
+    const double r0 = arakawa_rhs(wc.a, wc.b, wc.l, wp.a, wm.a, wp.b, wm.l, wp.l, wm.b,
+                                  sc.b, sc.l, sp.a, sm.a, sp.b, sm.l, sp.l, sm.b, k);
+    const double r1 = arakawa_rhs(wc.b, wc.r, wc.a, wp.b, wm.b, wp.r, wm.a, wp.a, wm.r,
+                                  sc.r, sc.a, sp.b, sm.b, sp.r, sm.a, sp.a, sm.r, k);
+    double2 o;
+    o.x = stage_update<STAGE>(r0, wc.a, wnv.x, k);
+    o.y = stage_update<STAGE>(r1, wc.b, wnv.y, k);
+    if (valid) *reinterpret_cast<double2*>(p.out + (size_t)y * nx + xs) = o;
+
+    wm = wc;
+    wc = wp;
+    sm = sc;
+    sc = sp;
+    wr_p = wr_n;
+    sr_p = sr_n;
+  }
+}
+
+__global__ __launch_bounds__(256) void divide_kernel(const DivideParams p) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = blockIdx.y;
+  if (i >= p.width) return;
+  const int kx = p.kx_off + i;
+  double2* ptr = p.spec + (size_t)j * p.pitch + i;
+  double2 o = make_double2(0.0, 0.0);
+  if (kx < p.nxh && !(kx == 0 && j == 0)) {  // e[1,1] = 0 (Common.jl:118); padding -> 0
+    double2 v = *ptr;
+    if (p.neg) {
+      v.x = -v.x;
+      v.y = -v.y;
+    }
+    const double d = (p.aa + p.bb * p.cx[kx]) + p.cc * p.cy[j];
+    o.x = (v.x / d) * p.scale;  // Julia Complex/Real: componentwise division
+    o.y = (v.y / d) * p.scale;
+  }
+  *ptr = o;
+}
+
+__global__ __launch_bounds__(256) void pack_kernel(const double2* __restrict__ X,
+                                                   double2* __restrict__ S, int nxh,
+                                                   int rows, int kb) {
+  const int kl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int jl = blockIdx.y;
+  const int q = blockIdx.z;
+  if (kl >= kb) return;
+  const int kx = q * kb + kl;
+  S[((size_t)q * rows + jl) * kb + kl] =
+      kx < nxh ? X[(size_t)jl * nxh + kx] : make_double2(0.0, 0.0);
+}
+
+__global__ __launch_bounds__(256) void unpack_kernel(const double2* __restrict__ S,
+                                                     double2* __restrict__ X, int nxh,
+                                                     int rows, int kb) {
+  const int kl = blockIdx.x * blockDim.x + threadIdx.x;
+  const int jl = blockIdx.y;
+  const int q = blockIdx.z;
+  const int kx = q * kb + kl;
+  if (kl >= kb || kx >= nxh) return;
+  X[(size_t)jl * nxh + kx] = S[((size_t)q * rows + jl) * kb + kl];
+}
+
+__global__ __launch_bounds__(256) void finite_kernel(const double* __restrict__ a, size_t n,
+                                                     int* flag) {
+  bool bad = false;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x)
+    bad |= !isfinite(a[i]);
+  if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
+}  // namespace
+
+void launch_stage(int stage, const StageParams& p, hipStream_t st) {
+  const int rpw = p.rows_per_wave;
+  dim3 grid((p.nx + kColsPerWave - 1) / kColsPerWave,
+            (p.ny + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw));
+  dim3 block(kWave * kWavesPerBlock);
+  switch (stage) {
+    case 0: hipLaunchKernelGGL(vm_stage_kernel<0>, grid, block, 0, st, p); break;
+    case 1: hipLaunchKernelGGL(vm_stage_kernel<1>, grid, block, 0, st, p); break;
+    case 2: hipLaunchKernelGGL(vm_stage_kernel<2>, grid, block, 0, st, p); break;
+    default: hipLaunchKernelGGL(vm_stage_kernel<3>, grid, block, 0, st, p); break;
+  }
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_divide(const DivideParams& p, hipStream_t st) {
+  dim3 grid((p.width + 255) / 256, p.rows);
+  hipLaunchKernelGGL(divide_kernel, grid, dim3(256), 0, st, p);
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_pack(const double2* X, double2* S, int nxh, int rows, int kb, int nranks,
+                 hipStream_t st) {
+  dim3 grid((kb + 255) / 256, rows, nranks);
+  hipLaunchKernelGGL(pack_kernel, grid, dim3(256), 0, st, X, S, nxh, rows, kb);
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_unpack(const double2* S, double2* X, int nxh, int rows, int kb, int nranks,
+                   hipStream_t st) {
+  dim3 grid((kb + 255) / 256, rows, nranks);
+  hipLaunchKernelGGL(unpack_kernel, grid, dim3(256), 0, st, S, X, nxh, rows, kb);
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_check_finite(const double* a, size_t n, int* flag, hipStream_t st) {
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  if (blocks == 0) blocks = 1;
+  hipLaunchKernelGGL(finite_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, n, flag);
+  CFDJ_HIP(hipGetLastError());
+}
+
+}  // namespace cfdj

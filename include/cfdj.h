@@ -1,0 +1,127 @@
+/*
+ * cfdj.h -- C ABI of libcfdj.so, the MI355X (gfx950) implementation of the
+ * t-bltg/CFD_Julia 2D vorticity-streamfunction Navier-Stokes hot path.
+ *
+ * The reference has no FFI: its "boundary" is a plain Julia call.  Each entry point
+ * below replaces one reference function (cited file:line, relative to the reference
+ * repository root) and keeps that function's argument meaning:
+ *
+ *   - arrays are caller-owned, column-major (x = Julia's first index is contiguous),
+ *     passed as (pointer, leading dimension in elements); a pointer may address any
+ *     element, e.g. &s[2,2] of a ghosted array, exactly as a Julia `pointer(s, k)`;
+ *   - host arrays are touched only during the call; every call that moves data
+ *     synchronises the handle's HIP stream before returning;
+ *   - device memory, rocFFT plans, HIP streams/events and RCCL communicators are owned
+ *     by the opaque handle;
+ *   - all functions return CFDJ_OK (0) or a negative CFDJ_ERR_* code; no C++ exception
+ *     crosses the ABI; cfdj_last_error() returns a thread-local message;
+ *   - one host thread per handle at a time.
+ *
+ * Julia binding: julia/CFDJ.jl.  Python binding: cfd_julia_amd/_lib.py (ctypes).
+ * See INTEGRATION.md.
+ */
+#ifndef CFDJ_H_
+#define CFDJ_H_
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CFDJ_OK 0
+#define CFDJ_ERR_ARG -1       /* bad size/pointer/argument (Julia: BoundsError, DivideError) */
+#define CFDJ_ERR_HIP -2       /* HIP runtime failure (out of memory, launch failure, ...) */
+#define CFDJ_ERR_ROCFFT -3    /* rocFFT plan/execute failure */
+#define CFDJ_ERR_RCCL -4      /* RCCL communicator / collective failure */
+#define CFDJ_ERR_NONFINITE -5 /* non-finite vorticity detected (optional check) */
+#define CFDJ_ERR_STATE -6     /* call not valid in the handle's current state */
+
+/* Kernel-category indices for cfdj_vm_timing(). */
+#define CFDJ_K_STAGE 0    /* fused Arakawa Jacobian + 5-pt Laplacian + RK3 stage kernel */
+#define CFDJ_K_FFT_FWD 1  /* rocFFT D2Z (forward real 2D / row transforms) */
+#define CFDJ_K_DIVIDE 2   /* spectral divide by the FD symbol (Common.jl:119-121) */
+#define CFDJ_K_FFT_INV 3  /* rocFFT Z2D (inverse) */
+#define CFDJ_K_COMM 4     /* halo exchange + FFT transposes (multi-GPU only) */
+#define CFDJ_K_COUNT 5
+
+typedef struct cfdj_vm cfdj_vm;   /* periodic vortex-merger solver state */
+typedef struct cfdj_fps_plan cfdj_fps_plan; /* periodic FD-FFT Poisson solver */
+
+/* ---- library ------------------------------------------------------------------ */
+const char* cfdj_last_error(void);
+const char* cfdj_version(void);
+/* Number of visible HIP devices (0 without a GPU; never fails). */
+int cfdj_device_count(void);
+
+/* ---- periodic FD-FFT Poisson: Common.jl:97-125 `fps`, fft_p.jl:8-42 `ps_fft` ------
+ * Solves  (u[i+1,j]-2u[i,j]+u[i-1,j])/dx^2 + (u[i,j+1]-2u[i,j]+u[i,j-1])/dy^2 = f
+ * on the periodic nx-by-ny grid with the reference's symbol
+ *   aa + bb*cos(kx_i) + cc*cos(ky_j),  kx[1] = eps,  ky = kx,  e[1,1] = 0.
+ * Requires nx even and ny <= nx (Common.jl:108,113).  The plan is built once per
+ * handle (the reference re-plans on every call). */
+int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device,
+                    cfdj_fps_plan** out);
+/* f: nx-by-ny host array (ldf >= nx) -> s: nx-by-ny host block (lds >= nx).
+ * Common.jl:97 writes s[2:nx+1, 2:ny+1]: pass &s[2,2] and lds = nx+2. */
+int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long lds);
+/* Same, on device pointers (contiguous, pitch nx) on the handle's stream; no sync. */
+int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
+void cfdj_fps_destroy(cfdj_fps_plan* h);
+/* One-shot convenience with the reference's per-call semantics. */
+int cfdj_fps(int nx, int ny, double dx, double dy, double eps, const double* f, long ldf,
+             double* s, long lds);
+
+/* ---- periodic vortex merger: vm.jl:12-90 `numerical`, Common.jl:132-182 `vm_rhs` --
+ * nx-by-ny periodic grid; re = Reynolds number; eps = the fps wavenumber guard (1e-6).
+ * device = HIP device ordinal (-1: current device). */
+int cfdj_vm_create(int nx, int ny, double dx, double dy, double re, double eps,
+                   int device, cfdj_vm** out);
+/* Multi-GPU y-slab variant (one process per GPU).  rank/nranks: this process's slot;
+ * nccl_id: 128-byte RCCL unique id from cfdj_comm_unique_id() on rank 0, broadcast by
+ * the host.  Rank p owns global rows [p*ny/nranks, (p+1)*ny/nranks).  ny % nranks == 0. */
+int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double eps,
+                        int device, int rank, int nranks, const void* nccl_id,
+                        cfdj_vm** out);
+int cfdj_comm_unique_id(void* out128);
+/* Virtual-rank variant for testing the slab decomposition on ONE GPU: nranks slabs,
+ * halo exchange and FFT transposes by device copies in one process. */
+int cfdj_vm_create_virtual(int nx, int ny, double dx, double dy, double re, double eps,
+                           int device, int nranks, cfdj_vm** out);
+
+/* Load the vorticity from a reference-layout ghosted (nx+2)-by-(ny+2) host array
+ * (vm.jl:117; ldw >= nx+2).  The interior w[2:nx+1, 2:ny+1] is authoritative; ghosts
+ * are periodic copies in every reference caller (vm.jl:121-128, tgv.jl:119-123).
+ * Distributed handles take the FULL global array on every rank and keep their slab. */
+int cfdj_vm_upload(cfdj_vm* h, const double* w, long ldw);
+/* Store the vorticity into a ghosted (nx+2)-by-(ny+2) host array, ghosts filled in the
+ * order of vm.jl:68-76.  Distributed handles: every rank receives the global field. */
+int cfdj_vm_download(cfdj_vm* h, double* w, long ldw);
+/* nsteps SSP-RK3 steps of size dt (vm.jl:24-87, without the text snapshots), fully
+ * device-resident; returns after the stream has drained. */
+int cfdj_vm_step(cfdj_vm* h, double dt, int nsteps);
+/* Enqueue nsteps steps without waiting (pair with cfdj_vm_sync). */
+int cfdj_vm_step_async(cfdj_vm* h, double dt, int nsteps);
+int cfdj_vm_sync(cfdj_vm* h);
+/* One vm_rhs (Common.jl:132-182) on a ghosted host array w: writes r[2:nx+1,2:ny+1]
+ * (ldr >= nx+2) and the whole ghosted s (lds >= nx+2, ghost order Common.jl:138-146).
+ * Single-GPU handles only. */
+int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, double* s,
+                long lds);
+/* Per-kernel-category device time (HIP events on the handle's stream).  enable != 0
+ * starts recording (and clears the counters); ms[CFDJ_K_COUNT] / launches[CFDJ_K_COUNT]
+ * receive the accumulated totals (either may be NULL). */
+int cfdj_vm_set_timing(cfdj_vm* h, int enable);
+int cfdj_vm_timing(cfdj_vm* h, double* ms, long* launches);
+/* Optional finiteness check of the vorticity after each cfdj_vm_step call. */
+int cfdj_vm_set_check_finite(cfdj_vm* h, int enable);
+/* Device pointer of this rank's nx-by-(ny/nranks) vorticity slab (pitch nx). */
+int cfdj_vm_field_device(cfdj_vm* h, double** w_dev);
+/* Shape of this rank's slab: global row offset and row count. */
+int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows);
+/* Tuning: rows marched by one wavefront in the stage kernel (default chosen per size). */
+int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
+void cfdj_vm_destroy(cfdj_vm* h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CFDJ_H_ */

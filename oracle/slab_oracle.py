@@ -1,0 +1,177 @@
+"""CPU restatement of the y-slab decomposed vortex-merger step (TEST INFRASTRUCTURE ONLY).
+
+The reference is single-process (no parallelism of any kind).  This module
+restates, in NumPy, the decomposition libcfdj.so implements for multi-GPU runs
+(cfd_julia_amd/csrc/cfdj_api.hip: cfdj_vm::poisson / halo / alltoall, pack/unpack
+kernels) so the CPU test suite can check its index arithmetic over real process groups
+(torch.distributed gloo, world_size >= 2) against the single-domain oracle:
+
+  rank p owns rows j in [p*rows, (p+1)*rows), rows = ny/P;
+  Poisson: row r2c along x -> pack S[q][jl][kl] = X[q*kb+kl, jl] (kb = ceil((nx/2+1)/P),
+  zero padded) -> all-to-all -> Y[y][kl] (y = p*rows + jl) -> c2c along y -> divide by the
+  symbol at global kx = rank*kb + kl -> inverse c2c -> all-to-all -> unpack -> c2r;
+  stencil: 1-row halos of omega and psi from ranks p-1 / p+1 (periodic).
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.fft as sfft
+
+from . import vm_oracle as vo
+
+
+class LocalComm:
+    """P virtual ranks in one process (lists of per-rank arrays)."""
+
+    def __init__(self, P):
+        self.P = P
+
+    def alltoall(self, chunks):
+        # chunks[p][q] (rank p's chunk for rank q) -> out[q][p]
+        P = self.P
+        return {q: [chunks[p][q] for p in range(P)] for q in range(P)}
+
+
+class DistComm:
+    """One rank of a torch.distributed process group (gloo on CPU)."""
+
+    def __init__(self):
+        import torch.distributed as dist
+        self.dist = dist
+        self.P = dist.get_world_size()
+        self.rank = dist.get_rank()
+        self.local_ranks = [self.rank]
+
+    def alltoall(self, chunks):
+        import torch
+        mine = chunks[self.rank]
+        shape = mine[0].shape
+        send = torch.from_numpy(np.ascontiguousarray(np.stack(mine)).view(np.float64).copy())
+        recv = torch.empty_like(send)
+        self.dist.all_to_all_single(recv.view(-1), send.view(-1))
+        arr = recv.numpy().view(np.complex128).reshape((self.P,) + shape)
+        return {self.rank: [arr[p] for p in range(self.P)]}
+
+    def halo(self, slabs):
+        import torch
+        (w,) = slabs
+        P, r = self.P, self.rank
+        prev, nxt = (r - 1) % P, (r + 1) % P
+        first = torch.from_numpy(np.ascontiguousarray(w[:, 0]))
+        last = torch.from_numpy(np.ascontiguousarray(w[:, -1]))
+        lo, hi = torch.empty_like(first), torch.empty_like(first)
+        # tags give the role, so prev == next (P = 2) is unambiguous
+        reqs = [self.dist.isend(first, prev, tag=1), self.dist.isend(last, nxt, tag=2),
+                self.dist.irecv(hi, nxt, tag=1), self.dist.irecv(lo, prev, tag=2)]
+        for q in reqs:
+            q.wait()
+        return [(lo.numpy(), hi.numpy())]
+
+
+def slab_layout(nx, ny, P):
+    if ny % P:
+        raise ValueError("ny must be divisible by P")
+    nxh = nx // 2 + 1
+    kb = -(-nxh // P)
+    return ny // P, nxh, kb
+
+
+def pack(X, P, kb):
+    """X (nxh, rows) -> S (P, rows, kb) with S[q, jl, kl] = X[q*kb+kl, jl] (0 padding)."""
+    nxh, rows = X.shape
+    S = np.zeros((P, rows, kb), dtype=np.complex128)
+    for q in range(P):
+        lo, hi = q * kb, min((q + 1) * kb, nxh)
+        if hi > lo:
+            S[q, :, :hi - lo] = X[lo:hi, :].T
+    return S
+
+
+def unpack(S, nxh):
+    P, rows, kb = S.shape
+    X = np.zeros((nxh, rows), dtype=np.complex128)
+    for q in range(P):
+        lo, hi = q * kb, min((q + 1) * kb, nxh)
+        if hi > lo:
+            X[lo:hi, :] = S[q, :, :hi - lo].T
+    return X
+
+
+def divide_block(Y, rank, kb, nx, ny, dx, dy, eps, neg):
+    """Y[y, kl] / symbol(kx = rank*kb + kl, y); padding and (0,0) -> 0 (Common.jl:118-121)."""
+    nxh = nx // 2 + 1
+    aa = -2.0 / (dx * dx) - 2.0 / (dy * dy)
+    bb = 2.0 / (dx * dx)
+    cc = 2.0 / (dy * dy)
+    ck = vo.cos_table(vo.kx_table(nx, eps))
+    kx = rank * kb + np.arange(kb)
+    valid = kx < nxh
+    cxv = np.where(valid, ck[np.minimum(kx, nxh - 1)], 1.0)
+    d = (aa + bb * cxv[None, :]) + cc * ck[:ny, None]
+    v = -Y if neg else Y
+    out = np.empty_like(Y)
+    out.real = v.real / d
+    out.imag = v.imag / d
+    out[:, ~valid] = 0.0
+    if rank == 0:
+        out[0, 0] = 0.0
+    return out
+
+
+def slab_poisson_all(w_slabs, nx, ny, dx, dy, eps, comm, neg=True, workers=1):
+    """psi slabs for all ranks of a LocalComm (or the single local rank of a DistComm)."""
+    P = comm.P
+    rows, nxh, kb = slab_layout(nx, ny, P)
+    ranks = getattr(comm, "local_ranks", list(range(P)))
+    S = {p: pack(sfft.rfft(w_slabs[i], axis=0, workers=workers), P, kb)
+         for i, p in enumerate(ranks)}
+    recv = comm.alltoall({p: [S[p][q] for q in range(P)] for p in ranks})
+    Ys = {}
+    for q in ranks:
+        Y = np.concatenate(recv[q], axis=0)  # (ny, kb): y = p*rows + jl
+        Y = sfft.fft(Y, axis=0, workers=workers)
+        Y = divide_block(Y, q, kb, nx, ny, dx, dy, eps, neg)
+        Ys[q] = sfft.ifft(Y, axis=0, workers=workers)
+    back = comm.alltoall({q: [Ys[q][p * rows:(p + 1) * rows] for p in range(P)]
+                          for q in ranks})
+    out = []
+    for p in ranks:
+        X = unpack(np.stack(back[p], axis=0), nxh)
+        out.append(sfft.irfft(X, n=nx, axis=0, workers=workers))
+    return out
+
+
+def halo_rows(slabs, comm):
+    """(lo, hi) ghost rows per local rank: lo = last row of p-1, hi = first row of p+1."""
+    if hasattr(comm, "halo"):
+        return comm.halo(slabs)
+    P = comm.P
+    return [(slabs[(p - 1) % P][:, -1], slabs[(p + 1) % P][:, 0]) for p in range(P)]
+
+
+def slab_rhs(w_slabs, psi_slabs, dx, dy, re, comm):
+    hw = halo_rows(w_slabs, comm)
+    hs = halo_rows(psi_slabs, comm)
+    out = []
+    for w, s, (wl, wh), (sl, sh) in zip(w_slabs, psi_slabs, hw, hs):
+        we = np.concatenate([wl[:, None], w, wh[:, None]], axis=1)
+        se = np.concatenate([sl[:, None], s, sh[:, None]], axis=1)
+        out.append(vo.arakawa_rhs(we, se, dx, dy, re)[:, 1:-1])
+    return out
+
+
+def slab_rk3_step(wn, dt, nx, ny, dx, dy, re, eps, comm):
+    def rhs(w):
+        return slab_rhs(w, slab_poisson_all(w, nx, ny, dx, dy, eps, comm), dx, dy, re, comm)
+
+    r = rhs(wn)
+    wt = [a + dt * b for a, b in zip(wn, r)]
+    r = rhs(wt)
+    wt = [(0.75 * a + 0.25 * b) + (0.25 * dt) * c for a, b, c in zip(wn, wt, r)]
+    r = rhs(wt)
+    return [(a / 3.0 + (2.0 / 3.0) * b) + ((2.0 / 3.0) * dt) * c for a, b, c in zip(wn, wt, r)]
+
+
+def split(w, P):
+    rows = w.shape[1] // P
+    return [np.array(w[:, p * rows:(p + 1) * rows]) for p in range(P)]

@@ -1,0 +1,259 @@
+"""GPU parity tests: libcfdj.so (through its C ABI) against the CPU oracle and the golden
+fixtures.  Tolerances (north star: vorticity L∞ < 1e-10 vs the reference CPU path):
+
+  * stencil / stage kernel given the same streamfunction: BIT-EXACT (both evaluate the
+    reference's expression order without FMA);
+  * FFT Poisson: rocFFT vs pocketfft round-off, |Δs| <= 1e-12 * max|s|;
+  * vorticity after K RK3 steps: L∞ < 1e-10 (absolute, |ω| ~ 1).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import vm_oracle as vo
+from tests.golden.make_golden import smooth_field
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def cfdj():
+    import cfd_julia_amd
+    from cfd_julia_amd import _lib
+
+    assert _lib.require_gpu() >= 1  # no silent fallback: the HIP library must run
+    return cfd_julia_amd
+
+
+def vm_setup(n):
+    dx, dy, x, y = vo.vm_grid(n, n)
+    return dx, dy, vo.vm_ic(n, n, x, y)
+
+
+# ---- Poisson ---------------------------------------------------------------------------
+@pytest.mark.parametrize("i", range(5))
+def test_gpu_fft_p_matches_order_jl(cfdj, i):
+    from cfd_julia_amd import fft_p
+
+    n = vo.ORDER_JL_GRID[i]
+    l2, _ = fft_p.main(grids=(n,))[n]
+    ref = vo.ORDER_JL_FFT_FDM[i]
+    assert abs(l2 - ref) / ref < 1e-10, (n, l2, ref)
+
+
+@pytest.mark.parametrize("n", [32, 64])
+def test_gpu_fps_golden(cfdj, golden, n):
+    z = golden(f"fps_mms_{n}")
+    with cfdj.PoissonFFT(n, n, float(z["dx"]), float(z["dy"])) as h:
+        s = h.solve(z["f"])
+    assert np.abs(s - z["s"]).max() <= 1e-12 * np.abs(z["s"]).max()
+
+
+@pytest.mark.parametrize("nx,ny", [(64, 64), (128, 128), (256, 256), (96, 96), (96, 64),
+                                   (200, 200), (8, 8)])
+def test_gpu_fps_vs_oracle(cfdj, nx, ny):
+    dx, dy, _, _ = vo.vm_grid(nx, ny)
+    f = smooth_field(nx, ny, 4, 11)
+    ref = vo.fps(f, dx, dy)
+    with cfdj.PoissonFFT(nx, ny, dx, dy) as h:
+        s = h.solve(np.asfortranarray(f))
+    assert np.abs(s - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+def test_gpu_common_fps_reference_signature(cfdj):
+    from cfd_julia_amd import common
+
+    nx = ny = 64
+    dx, dy, _, _ = vo.vm_grid(nx, ny)
+    f = np.asfortranarray(smooth_field(nx, ny, 4, 12))
+    s = np.zeros((nx + 2, ny + 2), order="F")
+    assert common.fps(nx, ny, dx, dy, None, None, None, None, f, s) is None
+    ref = vo.fps(f, dx, dy)
+    assert np.abs(s[1:-1, 1:-1] - ref).max() <= 1e-12 * np.abs(ref).max()
+    assert np.all(s[0, :] == 0) and np.all(s[:, 0] == 0)  # fps writes the interior only
+
+
+# ---- vm_rhs --------------------------------------------------------------------------------
+@pytest.mark.parametrize("name", ["vm_rhs_64x64", "vm_rhs_96x64"])
+def test_gpu_vm_rhs_golden(cfdj, golden, name):
+    z = golden(name)
+    nx, ny = z["w"].shape
+    with cfdj.VortexMerger(nx, ny, float(z["dx"]), float(z["dy"]), float(z["re"])) as h:
+        r, s = h.rhs(vo.to_ghosted(z["w"]))
+    smax = np.abs(z["s"]).max()
+    assert np.abs(s[1:-1, 1:-1] - z["s"]).max() <= 1e-12 * smax
+    assert np.abs(r[1:-1, 1:-1] - z["r"]).max() <= 1e-9 * np.abs(z["r"]).max()
+    # ghosts of s follow Common.jl:138-146 (periodic copies)
+    assert np.array_equal(s, vo.to_ghosted(s[1:-1, 1:-1]))
+
+
+@pytest.mark.parametrize("nx,ny", [(64, 64), (128, 128), (256, 256), (130, 130), (384, 256),
+                                   (16, 16), (6, 6)])
+def test_gpu_stencil_bit_exact_given_psi(cfdj, nx, ny):
+    """The fused Arakawa+Laplacian kernel reproduces the oracle's arakawa_rhs bit for bit
+    when both see the same streamfunction (here: the GPU's own s)."""
+    dx, dy, _, _ = vo.vm_grid(nx, ny)
+    w = smooth_field(nx, ny, 5, 21)
+    with cfdj.VortexMerger(nx, ny, dx, dy, 1000.0) as h:
+        r, s = h.rhs(vo.to_ghosted(w))
+    ref = vo.arakawa_rhs(w, s[1:-1, 1:-1], dx, dy, 1000.0)
+    assert np.array_equal(r[1:-1, 1:-1], ref), np.abs(r[1:-1, 1:-1] - ref).max()
+
+
+def test_gpu_common_vm_rhs_reference_signature(cfdj):
+    from cfd_julia_amd import common
+
+    nx = ny = 64
+    dx, dy, _, _ = vo.vm_grid(nx, ny)
+    w = vo.to_ghosted(smooth_field(nx, ny, 5, 22))
+    r = np.zeros_like(w)
+    s = np.zeros_like(w)
+    f = np.zeros((nx, ny), order="F")
+    common.vm_rhs(nx, ny, dx, dy, 1000.0, w, None, None, None, None, r, s, f)
+    rr, ss = vo.vm_rhs(w[1:-1, 1:-1], dx, dy, 1000.0)
+    assert np.array_equal(f, -w[1:-1, 1:-1])
+    assert np.abs(s[1:-1, 1:-1] - ss).max() <= 1e-12 * np.abs(ss).max()
+    assert np.abs(r[1:-1, 1:-1] - rr).max() <= 1e-9 * np.abs(rr).max()
+
+
+# ---- RK3 time loop -----------------------------------------------------------------------
+def test_gpu_vm_golden_10_steps(cfdj, golden):
+    z = golden("vm_64_10steps")
+    nx, ny = z["w0"].shape
+    with cfdj.VortexMerger(nx, ny, float(z["dx"]), float(z["dy"]), float(z["re"])) as h:
+        h.upload(vo.to_ghosted(z["w0"]))
+        h.step(float(z["dt"]), int(z["nt"]))
+        g = h.download()
+    assert np.abs(g[1:-1, 1:-1] - z["w10"]).max() < 1e-10
+    assert np.array_equal(g, vo.to_ghosted(g[1:-1, 1:-1]))  # vm.jl:68-76 ghosts
+
+
+@pytest.mark.parametrize("n,steps,dt", [(128, 20, 0.01), (256, 20, 0.005), (512, 10, 0.002),
+                                        (96, 20, 0.01)])
+def test_gpu_vm_steps_vs_oracle(cfdj, n, steps, dt):
+    dx, dy, w0 = vm_setup(n)
+    ref = vo.numerical(w0, steps, dt, dx, dy, 1000.0)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.upload_interior(w0)
+        h.step(dt, steps)
+        w = h.download_interior()
+    assert np.abs(w - ref).max() < 1e-10
+
+
+def test_gpu_vm_numerical_reference_signature(cfdj, tmp_path):
+    from cfd_julia_amd import vm
+
+    c = vm.setup(nx=64, ny=64, dt=0.01, tf=0.2, re=1000.0, ns=2)
+    wn = c["wn"]
+    w0 = np.array(wn[1:-1, 1:-1])
+    un = vm.numerical(c["nx"], c["ny"], c["nt"], c["dx"], c["dy"], c["dt"], c["re"], c["x"],
+                      c["y"], wn, c["ns"], outdir=str(tmp_path))
+    ref = vo.numerical(w0, c["nt"], c["dt"], c["dx"], c["dy"], c["re"])
+    assert un.shape == (65, 65)
+    assert np.abs(un[:64, :64] - ref).max() < 1e-10
+    assert np.array_equal(wn[1:-1, 1:-1], un[:64, :64])  # wn mutated in place
+    # vm.jl:78-86 writes vm1.txt (m never incremented) with (nx+1)^2 "x y ω" lines
+    lines = open(tmp_path / "vm1.txt").read().splitlines()
+    assert len(lines) == 65 * 65
+    x, y, val = map(float, lines[1].split())
+    assert x == c["x"][1] and y == c["y"][0] and val == un[1, 0]
+    assert not (tmp_path / "vm2.txt").exists()
+
+
+def test_gpu_tgv_known_answer(cfdj, golden):
+    def stepper(w0, nt, dt, dx, dy, re):
+        with cfdj.VortexMerger(w0.shape[0], w0.shape[1], dx, dy, re) as h:
+            h.upload_interior(w0)
+            h.step(dt, nt)
+            return h.download_interior()
+
+    l2, linf = vo.tgv_error(64, 10.0, 0.01, 1.0, stepper=stepper)
+    z = golden("tgv_64")
+    assert abs(l2 - float(z["l2"])) < 1e-12 and abs(linf - float(z["linf"])) < 1e-12
+
+
+def test_gpu_conservation_at_full_size(cfdj):
+    """C3 size (4096^2): Arakawa + periodic Laplacian + FD Poisson conserve the mean
+    vorticity exactly in exact arithmetic -> drift must be round-off only."""
+    n = 4096
+    dx, dy, w0 = vm_setup(n)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.set_check_finite(True)
+        h.upload_interior(w0)
+        h.step(5e-4, 10)
+        w = h.download_interior()
+    assert abs(w.mean() - w0.mean()) < 1e-12
+    assert 0.99 < w.max() <= w0.max() + 1e-12
+
+
+def test_gpu_full_size_vs_oracle(cfdj):
+    """C3 (4096^2, re = 1000, dt = 5e-4): L∞ vs the oracle after 3 RK3 steps."""
+    n = 4096
+    dx, dy, w0 = vm_setup(n)
+    ref = vo.numerical(w0, 3, 5e-4, dx, dy, 1000.0)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.upload_interior(w0)
+        h.step(5e-4, 3)
+        w = h.download_interior()
+    assert np.abs(w - ref).max() < 1e-10
+
+
+# ---- y-slab decomposition (virtual ranks on one GPU) ---------------------------------------
+@pytest.mark.parametrize("P,n", [(1, 64), (2, 64), (4, 128), (8, 128), (3, 96)])
+def test_gpu_virtual_slabs_vs_single(cfdj, P, n):
+    dx, dy, w0 = vm_setup(n)
+    ref = vo.numerical(w0, 5, 0.01, dx, dy, 1000.0)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+        h.upload_interior(w0)
+        h.step(0.01, 5)
+        w = h.download_interior()
+    assert np.abs(w - ref).max() < 1e-10
+
+
+# ---- robustness ----------------------------------------------------------------------------
+def test_gpu_input_field_preserved_by_forward_fft(cfdj):
+    nx = ny = 256
+    dx, dy, _, _ = vo.vm_grid(nx, ny)
+    f = np.asfortranarray(smooth_field(nx, ny, 4, 31))
+    with cfdj.PoissonFFT(nx, ny, dx, dy) as h:
+        a = h.solve(f)
+        b = h.solve(f)
+    assert np.array_equal(a, b)
+
+
+def test_gpu_nonfinite_detected(cfdj):
+    n = 256
+    dx, dy, w0 = vm_setup(n)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.set_check_finite(True)
+        h.upload_interior(w0)
+        with pytest.raises(cfdj.CfdjError) as e:
+            h.step(0.5, 200)  # far beyond the RK3 viscous limit -> blows up
+        assert e.value.code == -5
+
+
+def test_gpu_timing_counters(cfdj):
+    n = 256
+    dx, dy, w0 = vm_setup(n)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.upload_interior(w0)
+        h.set_timing(True)
+        h.step(0.001, 4)
+        t = h.timing()
+    assert t["stage"][1] == 12 and t["fft_fwd"][1] == 12 and t["divide"][1] == 12
+    assert all(v[0] > 0 for k, v in t.items() if k != "comm")
+
+
+@pytest.mark.parametrize("rpw", [1, 3, 8, 64, 1000])
+def test_gpu_rows_per_wave_invariance(cfdj, rpw):
+    n = 192
+    dx, dy, w0 = vm_setup(n)
+    outs = []
+    for r in (rpw, 16):
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+            h.set_rows_per_wave(r)
+            h.upload_interior(w0)
+            h.step(0.01, 2)
+            outs.append(h.download_interior())
+    assert np.array_equal(outs[0], outs[1])
