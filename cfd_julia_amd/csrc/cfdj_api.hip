@@ -92,6 +92,7 @@ struct Symbol {
   double aa = 0, bb = 0, cc = 0, scale = 0;
   double* cx = nullptr;  // cos(kx[m]), m < nxh
   double* cy = nullptr;  // cos(ky[n]) = cos(kx[n]), n < ny
+  double* cy_mirror = nullptr;  // ny < nx: cos(ky[(ny - n) % ny]) (see DivideParams)
   void init(int nx_, int ny_, double dx, double dy, double eps) {
     nx = nx_;
     ny = ny_;
@@ -107,10 +108,17 @@ struct Symbol {
     cy = dalloc<double>(ny);
     CFDJ_HIP(hipMemcpy(cx, hcx.data(), nxh * sizeof(double), hipMemcpyHostToDevice));
     CFDJ_HIP(hipMemcpy(cy, hcy.data(), ny * sizeof(double), hipMemcpyHostToDevice));
+    if (ny != nx) {
+      std::vector<double> hm(ny);
+      for (int n = 0; n < ny; ++n) hm[n] = hcy[(ny - n) % ny];
+      cy_mirror = dalloc<double>(ny);
+      CFDJ_HIP(hipMemcpy(cy_mirror, hm.data(), ny * sizeof(double), hipMemcpyHostToDevice));
+    }
   }
   void destroy() {
     dfree(cx);
     dfree(cy);
+    dfree(cy_mirror);
   }
   DivideParams divide(double2* spec, int width, int rows, int pitch, int kx_off,
                       bool neg) const {
@@ -118,6 +126,7 @@ struct Symbol {
     p.spec = spec;
     p.cx = cx;
     p.cy = cy;
+    p.cy_mirror = cy_mirror;
     p.width = width;
     p.rows = rows;
     p.pitch = pitch;

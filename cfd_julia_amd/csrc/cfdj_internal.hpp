@@ -83,6 +83,10 @@ struct DivideParams {
   double2* spec;
   const double* cx;  // cos(kx[m]), m = 0..nxh-1
   const double* cy;  // cos(ky[n]), n = 0..ny-1
+  // ny < nx only: cos(ky[(ny-n) mod ny]).  Common.jl:113 aliases ky = kx, so for ny < nx
+  // the symbol is not Hermitian in y and the reference's real(ifft(e/d)) equals the
+  // c2r of e * (1/d(m,n) + 1/d(-m,-n))/2; NULL when ny == nx (plain division).
+  const double* cy_mirror;
   int width, rows, pitch, kx_off, nxh;
   double aa, bb, cc, scale;
   bool neg;

@@ -157,9 +157,16 @@ __global__ __launch_bounds__(256) void divide_kernel(const DivideParams p) {
       v.x = -v.x;
       v.y = -v.y;
     }
-    const double d = (p.aa + p.bb * p.cx[kx]) + p.cc * p.cy[j];
-    o.x = (v.x / d) * p.scale;  // Julia Complex/Real: componentwise division
-    o.y = (v.y / d) * p.scale;
+    const double ax = p.aa + p.bb * p.cx[kx];
+    const double d = ax + p.cc * p.cy[j];
+    if (p.cy_mirror == nullptr) {
+      o.x = (v.x / d) * p.scale;  // Julia Complex/Real: componentwise division
+      o.y = (v.y / d) * p.scale;
+    } else {
+      const double d2 = ax + p.cc * p.cy_mirror[j];
+      o.x = (0.5 * (v.x / d + v.x / d2)) * p.scale;
+      o.y = (0.5 * (v.y / d + v.y / d2)) * p.scale;
+    }
   }
   *ptr = o;
 }
