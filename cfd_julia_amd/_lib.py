@@ -21,6 +21,7 @@ ERR_NAMES = {-1: "CFDJ_ERR_ARG", -2: "CFDJ_ERR_HIP", -3: "CFDJ_ERR_ROCFFT",
              -4: "CFDJ_ERR_RCCL", -5: "CFDJ_ERR_NONFINITE", -6: "CFDJ_ERR_STATE"}
 K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
+POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED = 0, 1, 2
 
 
 class CfdjError(RuntimeError):
@@ -71,6 +72,9 @@ SIGNATURES = {
     "cfdj_vm_field_device": (C.c_int, [_vp, C.POINTER(_vp)]),
     "cfdj_vm_slab": (C.c_int, [_vp, _ip, _ip]),
     "cfdj_vm_set_rows_per_wave": (C.c_int, [_vp, C.c_int]),
+    "cfdj_vm_set_poisson": (C.c_int, [_vp, C.c_int]),
+    "cfdj_vm_get_poisson": (C.c_int, [_vp]),
+    "cfdj_fps_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_destroy": (None, [_vp]),
 }
 

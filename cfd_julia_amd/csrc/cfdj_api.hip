@@ -182,6 +182,63 @@ struct Plans {
   }
 };
 
+// exp(-2 pi i k / n), k < n, rounded from long double (x86 80-bit) arithmetic.
+static double2* twiddle_table(int n) {
+  const long double pi = 3.141592653589793238462643383279502884L;
+  std::vector<double2> h(n);
+  for (int k = 0; k < n; ++k) {
+    const long double a = 2.0L * pi * (long double)k / (long double)n;
+    h[k] = make_double2((double)cosl(a), (double)-sinl(a));
+  }
+  double2* d = dalloc<double2>(n);
+  CFDJ_HIP(hipMemcpy(d, h.data(), n * sizeof(double2), hipMemcpyHostToDevice));
+  return d;
+}
+
+// Hand-written 3-pass FFT Poisson (poisson_fft.hip) state: twiddle tables.
+struct Fused {
+  int n = 0;
+  double2* twL = nullptr;
+  double2* twN = nullptr;
+  void init(int n_) {
+    n = n_;
+    twL = twiddle_table(n / 2);
+    twN = twiddle_table(n);
+  }
+  void destroy() {
+    dfree(twL);
+    dfree(twN);
+  }
+  FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H,
+                        bool neg) const {
+    FusedPoissonArgs a;
+    a.n = n;
+    a.f = f;
+    a.s = s;
+    a.H = H;
+    a.twL = twL;
+    a.twN = twN;
+    a.cx = sym.cx;
+    a.cy = sym.cy;
+    a.aa = sym.aa;
+    a.bb = sym.bb;
+    a.cc = sym.cc;
+    a.scale = sym.scale;
+    a.neg = neg;
+    return a;
+  }
+};
+
+// Poisson path selection (cfdj_vm_set_poisson / cfdj_fps_set_poisson).
+static bool resolve_fused(int path, int nx, int ny, bool slab) {
+  if (path == CFDJ_POISSON_ROCFFT) return false;
+  const bool ok = !slab && fused_poisson_supported(nx, ny);
+  if (path == CFDJ_POISSON_FUSED && !ok)
+    throw Error{CFDJ_ERR_ARG, "fused Poisson needs a single-GPU square grid of 1024, 2048 "
+                              "or 4096 points per side"};
+  return ok;
+}
+
 }  // namespace cfdj
 
 using namespace cfdj;
@@ -197,13 +254,21 @@ struct cfdj_fps_plan {
   rocfft_plan fwd = nullptr, inv = nullptr;
   double2* spec = nullptr;
   double *f_dev = nullptr, *s_dev = nullptr;
+  Fused fused;
+  bool use_fused = false;
 
   void solve_device(const double* f, double* s) {
+    if (use_fused) {
+      const FusedPoissonArgs a = fused.args(sym, f, s, spec, false);
+      for (int pass = 0; pass < 3; ++pass) launch_fused_poisson_pass(pass, a, stream);
+      return;
+    }
     plans.exec(fwd, f, spec);
     launch_divide(sym.divide(spec, sym.nxh, sym.ny, sym.nxh, 0, false), stream);
     plans.exec(inv, spec, s);
   }
   ~cfdj_fps_plan() {
+    fused.destroy();
     plans.destroy();
     sym.destroy();
     dfree(spec);
@@ -252,6 +317,8 @@ struct cfdj_vm {
   rocfft_plan fwd2d = nullptr, inv2d = nullptr;                  // Single
   rocfft_plan row_fwd = nullptr, row_inv = nullptr, col_fwd = nullptr, col_inv = nullptr;
   double2* spec = nullptr;                                       // Single
+  Fused fused;                                                   // Single, 2^k grids
+  bool use_fused = false;
   ncclComm_t comm = nullptr;
   double* gather = nullptr;                                      // Rccl download buffer
   // timing
@@ -355,6 +422,16 @@ struct cfdj_vm {
 
   // ---- Poisson: psi = fps(-w)  (Common.jl:134-136) ------------------------------------
   void poisson(const std::vector<const double*>& src, bool neg) {
+    if (!slab_mode() && use_fused) {
+      const FusedPoissonArgs a = fused.args(sym, src[0], slabs[0].psi, spec, neg);
+      static const int cat[3] = {CFDJ_K_FFT_FWD, CFDJ_K_DIVIDE, CFDJ_K_FFT_INV};
+      for (int pass = 0; pass < 3; ++pass) {
+        tbegin(cat[pass]);
+        launch_fused_poisson_pass(pass, a, stream);
+        tend();
+      }
+      return;
+    }
     if (!slab_mode()) {
       Slab& s = slabs[0];
       tbegin(CFDJ_K_FFT_FWD);
@@ -525,6 +602,10 @@ struct cfdj_vm {
     }
     plans.finalize(stream);
     d_flag = dalloc<int>(1);
+    if (!slab_mode() && fused_poisson_supported(nx, ny)) {
+      fused.init(nx);
+      use_fused = true;
+    }
   }
 
   ~cfdj_vm() {
@@ -532,6 +613,7 @@ struct cfdj_vm {
     for (auto& s : slabs) s.destroy();
     plans.destroy();
     sym.destroy();
+    fused.destroy();
     dfree(spec);
     dfree(gather);
     dfree(d_flag);
@@ -631,6 +713,10 @@ int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device
     h->spec = dalloc<double2>((size_t)h->sym.nxh * ny);
     h->f_dev = dalloc<double>((size_t)nx * ny);
     h->s_dev = dalloc<double>((size_t)nx * ny);
+    if (fused_poisson_supported(nx, ny)) {
+      h->fused.init(nx);
+      h->use_fused = true;
+    }
     *out = h.release();
   });
 }
@@ -868,6 +954,33 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
     CFDJ_REQUIRE(rows >= 1, "rows must be >= 1");
     h->rows_per_wave = rows;
+  });
+}
+
+int cfdj_vm_set_poisson(cfdj_vm* h, int path) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(path >= CFDJ_POISSON_AUTO && path <= CFDJ_POISSON_FUSED, "bad path");
+    select_device(h->device);
+    const bool f = resolve_fused(path, h->nx, h->ny, h->slab_mode());
+    if (f && !h->fused.twN) h->fused.init(h->nx);
+    h->use_fused = f;
+  });
+}
+
+int cfdj_vm_get_poisson(cfdj_vm* h) {
+  if (!h) return CFDJ_ERR_ARG;
+  return h->use_fused ? CFDJ_POISSON_FUSED : CFDJ_POISSON_ROCFFT;
+}
+
+int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(path >= CFDJ_POISSON_AUTO && path <= CFDJ_POISSON_FUSED, "bad path");
+    select_device(h->device);
+    const bool f = resolve_fused(path, h->sym.nx, h->sym.ny, false);
+    if (f && !h->fused.twN) h->fused.init(h->sym.nx);
+    h->use_fused = f;
   });
 }
 

@@ -101,6 +101,24 @@ void launch_pack(const double2* X, double2* S, int nxh, int rows, int kb, int nr
 void launch_unpack(const double2* S, double2* X, int nxh, int rows, int kb, int nranks,
                    hipStream_t st);
 
+// Hand-written fused FD-FFT Poisson for square power-of-two grids (poisson_fft.hip):
+// pass 0 = row r2c (f -> column-tiled packed half spectrum H), pass 1 = per-tile column
+// FFT + divide + inverse FFT (in place on H), pass 2 = row c2r (H -> s).
+struct FusedPoissonArgs {
+  int n;                // nx == ny
+  const double* f;      // input field (pitch n)
+  double* s;            // output streamfunction (pitch n)
+  double2* H;           // (n/2) x n complex work spectrum
+  const double2* twL;   // exp(-2 pi i k/(n/2)), k < n/2
+  const double2* twN;   // exp(-2 pi i k/n), k < n
+  const double* cx;     // cos(kx[m]), m <= n/2
+  const double* cy;     // cos(ky[k]), k < n
+  double aa, bb, cc, scale;
+  bool neg;
+};
+bool fused_poisson_supported(int nx, int ny);
+void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);
+
 // Finiteness check: sets *flag = 1 if any element is not finite.
 void launch_check_finite(const double* a, size_t n, int* flag, hipStream_t st);
 

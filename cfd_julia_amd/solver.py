@@ -8,6 +8,8 @@ import numpy as np
 from . import _lib
 from ._lib import check, dptr
 
+_PATHS = {"auto": _lib.POISSON_AUTO, "rocfft": _lib.POISSON_ROCFFT, "fused": _lib.POISSON_FUSED}
+
 
 class PoissonFFT:
     """Periodic FD-FFT Poisson solver, plan built once (Common.jl:97-125 `fps`,
@@ -31,6 +33,10 @@ class PoissonFFT:
         check(_lib.load().cfdj_fps_solve(self._h, dptr(f), ldf, dptr(out), lds),
               "cfdj_fps_solve")
         return out
+
+    def set_poisson(self, path):
+        """path: "auto" | "rocfft" | "fused" (CFDJ_POISSON_*)."""
+        check(_lib.load().cfdj_fps_set_poisson(self._h, _PATHS[path]), "cfdj_fps_set_poisson")
 
     def solve_device(self, f_ptr, s_ptr):
         check(_lib.load().cfdj_fps_solve_device(self._h, C.c_void_p(f_ptr), C.c_void_p(s_ptr)),
@@ -147,6 +153,14 @@ class VortexMerger:
     def set_rows_per_wave(self, rows):
         check(_lib.load().cfdj_vm_set_rows_per_wave(self._h, int(rows)),
               "cfdj_vm_set_rows_per_wave")
+
+    def set_poisson(self, path):
+        """path: "auto" | "rocfft" | "fused" (CFDJ_POISSON_*)."""
+        check(_lib.load().cfdj_vm_set_poisson(self._h, _PATHS[path]), "cfdj_vm_set_poisson")
+
+    def poisson(self):
+        return {_lib.POISSON_FUSED: "fused", _lib.POISSON_ROCFFT: "rocfft"}[
+            _lib.load().cfdj_vm_get_poisson(self._h)]
 
     def field_device_ptr(self):
         p = C.c_void_p()

@@ -43,6 +43,11 @@ extern "C" {
 #define CFDJ_K_COMM 4     /* halo exchange + FFT transposes (multi-GPU only) */
 #define CFDJ_K_COUNT 5
 
+/* Poisson implementation (cfdj_vm_set_poisson / cfdj_fps_set_poisson). */
+#define CFDJ_POISSON_AUTO 0   /* fused where supported, rocFFT otherwise (default) */
+#define CFDJ_POISSON_ROCFFT 1 /* rocFFT D2Z + divide kernel + rocFFT Z2D */
+#define CFDJ_POISSON_FUSED 2  /* hand-written 3-pass FFT (square 1024/2048/4096 grids) */
+
 typedef struct cfdj_vm cfdj_vm;   /* periodic vortex-merger solver state */
 typedef struct cfdj_fps_plan cfdj_fps_plan; /* periodic FD-FFT Poisson solver */
 
@@ -65,6 +70,8 @@ int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device
 int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long lds);
 /* Same, on device pointers (contiguous, pitch nx) on the handle's stream; no sync. */
 int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
+/* Select the Poisson implementation (CFDJ_POISSON_*); ARG error if unsupported. */
+int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path);
 void cfdj_fps_destroy(cfdj_fps_plan* h);
 /* One-shot convenience with the reference's per-call semantics. */
 int cfdj_fps(int nx, int ny, double dx, double dy, double eps, const double* f, long ldf,
@@ -119,6 +126,9 @@ int cfdj_vm_field_device(cfdj_vm* h, double** w_dev);
 int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows);
 /* Tuning: rows marched by one wavefront in the stage kernel (default chosen per size). */
 int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
+/* Select / query the Poisson implementation (CFDJ_POISSON_*; single-GPU handles). */
+int cfdj_vm_set_poisson(cfdj_vm* h, int path);
+int cfdj_vm_get_poisson(cfdj_vm* h);
 void cfdj_vm_destroy(cfdj_vm* h);
 
 #ifdef __cplusplus

@@ -257,3 +257,60 @@ def test_gpu_rows_per_wave_invariance(cfdj, rpw):
             h.step(0.01, 2)
             outs.append(h.download_interior())
     assert np.array_equal(outs[0], outs[1])
+
+
+# ---- hand-written fused FFT Poisson (poisson_fft.hip) -------------------------------------
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
+def test_gpu_fused_fps_vs_oracle_and_rocfft(cfdj, n):
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    f = np.asfortranarray(smooth_field(n, n, 3, 41) + 0.01 * np.random.default_rng(n)
+                          .standard_normal((n, n)))
+    ref = vo.fps(f, dx, dy)
+    with cfdj.PoissonFFT(n, n, dx, dy) as h:
+        h.set_poisson("fused")
+        s_f = h.solve(f)
+        h.set_poisson("rocfft")
+        s_r = h.solve(f)
+    scale = np.abs(ref).max()
+    assert np.abs(s_r - ref).max() <= 1e-12 * scale
+    assert np.abs(s_f - ref).max() <= 1e-12 * scale, np.abs(s_f - ref).max() / scale
+
+
+@pytest.mark.parametrize("n", [1024, 2048])
+def test_gpu_fused_fft_p_mms(cfdj, n):
+    # fft_p.jl MMS error at larger N: the fused path reaches the FD truncation error
+    from cfd_julia_amd import fft_p
+
+    f, ue, dx, dy = fft_p.mms(n)
+    with cfdj.PoissonFFT(n, n, dx, dy) as h:
+        h.set_poisson("fused")
+        un = np.zeros_like(f)
+        un[:n, :n] = h.solve(f[:n, :n])
+    un[n, :] = un[0, :]
+    un[:, n] = un[:, 0]
+    l2, _ = vo.fft_p_mms_error(n)
+    l2g = math.sqrt(float(np.sum((un - ue) ** 2)) / un.size)
+    assert abs(l2g - l2) / l2 < 1e-9
+
+
+@pytest.mark.parametrize("n,steps", [(1024, 10), (2048, 4)])
+def test_gpu_fused_vm_steps_vs_oracle(cfdj, n, steps):
+    dx, dy, w0 = vm_setup(n)
+    dt = 5e-4 * (4096 / n) ** 2
+    ref = vo.numerical(w0, steps, dt, dx, dy, 1000.0)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        assert h.poisson() == "fused"
+        h.upload_interior(w0)
+        h.step(dt, steps)
+        w = h.download_interior()
+    assert np.abs(w - ref).max() < 1e-10
+
+
+def test_gpu_poisson_path_selection(cfdj):
+    dx, dy, _ = vm_setup(64)
+    with cfdj.VortexMerger(64, 64, dx, dy, 1000.0) as h:
+        assert h.poisson() == "rocfft"
+        with pytest.raises(cfdj.ArgumentError):
+            h.set_poisson("fused")
+    with cfdj.VortexMerger(1024, 1024, dx, dy, 1000.0, kind="virtual", nranks=2) as h:
+        assert h.poisson() == "rocfft"
