@@ -197,11 +197,14 @@ static double2* twiddle_table(int n) {
 
 // Hand-written 3-pass FFT Poisson (poisson_fft.hip) state: twiddle tables.
 struct Fused {
-  int n = 0;
+  int n = 0, ncu = 256;
   double2* twL = nullptr;
   double2* twN = nullptr;
   void init(int n_) {
     n = n_;
+    int dev = 0;
+    CFDJ_HIP(hipGetDevice(&dev));
+    CFDJ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
     twL = twiddle_table(n / 2);
     twN = twiddle_table(n);
   }
@@ -225,6 +228,7 @@ struct Fused {
     a.cc = sym.cc;
     a.scale = sym.scale;
     a.neg = neg;
+    a.ncu = ncu;
     return a;
   }
 };
@@ -649,7 +653,7 @@ cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int
   h->nranks = nranks;
   h->rank = rank;
   // rows per wavefront: keep >= ~8 waves per CU at the benchmark sizes
-  h->rows_per_wave = ny / nranks >= 2048 ? 16 : 8;
+  h->rows_per_wave = ny / nranks >= 2048 ? 32 : 8;  // r01 sweep: 32 best at 4096^2
   CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   if (mode == Mode::Virtual) {
     h->slabs.resize(nranks);

@@ -48,6 +48,20 @@ struct Error {
     if (!(cond)) throw ::cfdj::Error{CFDJ_ERR_ARG, (msg)};                              \
   } while (0)
 
+// ---- XCD-aware block order ------------------------------------------------------------
+// Workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8 share an XCD and its
+// L2; MI355X_MICROARCH.md, Workgroup dispatch).  xcd_remap gives each XCD a contiguous
+// range of the logical work index so neighbouring tiles (which share cache lines: 64-B
+// halves of a 128-B line, stencil edge columns and halo rows) meet in the same L2.
+// Bijective for any n; speed only, never correctness.
+__device__ __forceinline__ int xcd_remap(int b, int n) {
+  constexpr int X = 8;
+  const int q = n / X, r = n % X;  // XCD x gets q + (x < r) consecutive logical indices
+  const int x = b % X, slot = b / X;
+  if (slot >= q + (x < r ? 1 : 0)) return b;  // cannot happen for b < n
+  return x * q + (x < r ? x : r) + slot;
+}
+
 // ---- kernel parameter blocks --------------------------------------------------------
 // Constants of Common.jl:149-152 plus the RK3 stage weights of vm.jl:28,43-47,62-66.
 struct StageCoef {
@@ -115,6 +129,7 @@ struct FusedPoissonArgs {
   const double* cy;     // cos(ky[k]), k < n
   double aa, bb, cc, scale;
   bool neg;
+  int ncu;              // compute units (persistent grid size)
 };
 bool fused_poisson_supported(int nx, int ny);
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);

@@ -7,10 +7,11 @@
 //                f[2n] + i f[2n+1], FFT'd (length L = N/2, Stockham radix-16 in LDS), and
 //                post-processed into the real-FFT half spectrum X[m], m = 0..L-1, with the
 //                two real coefficients X[0] (DC) and X[L] (Nyquist) packed into slot 0 as
-//                X[0] + i X[L].  Output is written COLUMN-TILED: tile t holds columns
-//                m = 2t, 2t+1 for all rows, H[t][y][c] (32 B per row, 128 KB per tile), so
-//                the column pass reads one contiguous block.
-//   cols       : one workgroup per 2-column tile: forward FFT along y (length M), the
+//                X[0] + i X[L].  Output is written COLUMN-MAJOR, H[m][y] (y contiguous):
+//                a workgroup owns XR = 4 consecutive rows, so every column piece it writes
+//                is a full 64-B segment, and the column pass reads one contiguous 64 KB
+//                column.
+//   cols       : one workgroup per column: forward FFT along y (length M), the
 //                spectral divide by the FD symbol aa + bb cos kx + cc cos ky (Common.jl:119-
 //                121; packed column 0 is split into its DC and Nyquist halves with the
 //                Z[k], Z[-k] symmetry, each divided by its own symbol), the inverse FFT, all
@@ -152,7 +153,7 @@ struct Plan {
   static constexpr int radix(int s) { return s < N16 ? 16 : REM; }
   static constexpr int ns(int s) { return s == 0 ? 1 : ns(s - 1) * radix(s - 1); }
   static constexpr int PAD = L + L / 16;  // LDS elements per transform (1 pad per 16)
-  static constexpr int ROWSTRIDE = PAD + 2;  // rows kernels: stagger banks between rows
+  static constexpr int ROWSTRIDE = PAD;  // rows kernels: row stride (= 0 mod 64 banks)
 };
 
 __device__ __forceinline__ int padx(int i) { return i + (i >> 4); }
@@ -169,20 +170,45 @@ __device__ __forceinline__ double fd_symbol(double ax, double cc, double cy) {
   return ax + cc * cy;
 }
 
-// Twiddles of one butterfly: w[0] = W^e, w[1] = W^{4e} (R >= 8) for the stage's base
-// exponent e = (j mod NS) * L/(NS*R); tw[i] = exp(-2 pi i i / L).  Loaded early (before the
-// stage's LDS reads and barrier) so the L2 latency overlaps them.
+// Twiddles live in LDS as a 2-level table, W_L^e = hi[e >> 6] * lo[e & 63] (one rounding),
+// filled once per persistent workgroup from the host-built long-double tables.  Keeping
+// them out of the vector-memory stream matters: vmcnt is in order, so a twiddle load issued
+// behind the next item's HBM prefetch would wait for that whole prefetch.
+template <int L>
+struct TwLds {
+  static constexpr int HI = L / 64 > 0 ? L / 64 : 1;
+  double2 lo[64];
+  double2 hi[HI];
+  __device__ __forceinline__ void fill(const double2* __restrict__ tw) {
+    for (int i = threadIdx.x; i < 64 + HI; i += blockDim.x) {
+      if (i < 64) lo[i] = tw[i];
+      else hi[i - 64] = tw[(i - 64) * 64];
+    }
+  }
+  __device__ __forceinline__ double2 w(int e) const { return cmul(hi[e >> 6], lo[e & 63]); }
+};
+
+// The same interface over the global long-double table (L2-resident): used where no HBM
+// prefetch is queued ahead of the twiddle loads (the non-persistent column pass).
+template <int L>
+struct TwGlobal {
+  const double2* __restrict__ t;
+  __device__ __forceinline__ double2 w(int e) const { return t[e]; }
+};
+
+// Twiddles of one butterfly: w1 = W^e, w4 = W^{4e} (R >= 8) for the stage's base exponent
+// e = (j mod NS) * L/(NS*R).
 template <int L, int R, int NS>
 struct Tw {
   double2 w1, w4;
 };
-template <int L, int R, int NS>
-__device__ __forceinline__ Tw<L, R, NS> load_tw(int j, const double2* __restrict__ tw) {
+template <int L, int R, int NS, class TW>
+__device__ __forceinline__ Tw<L, R, NS> load_tw(int j, const TW& tw) {
   Tw<L, R, NS> t;
   if constexpr (NS > 1) {
     const int e = (j & (NS - 1)) * (L / (NS * R));
-    t.w1 = tw[e];
-    if constexpr (R >= 8) t.w4 = tw[4 * e];
+    t.w1 = tw.w(e);
+    if constexpr (R >= 8) t.w4 = tw.w(4 * e);
   }
   return t;
 }
@@ -230,12 +256,12 @@ struct StageTw {
   static constexpr int NS = Plan<L>::ns(S);
   Tw<L, R, NS> t[16 / R];
 };
-template <int L, int S>
-__device__ __forceinline__ StageTw<L, S> stage_tw(int tid, const double2* __restrict__ tw) {
+template <int L, int S, class TW>
+__device__ __forceinline__ StageTw<L, S> stage_tw(int tid, const TW& tw) {
   StageTw<L, S> st;
 #pragma unroll
   for (int b = 0; b < 16 / StageTw<L, S>::R; ++b)
-    st.t[b] = load_tw<L, StageTw<L, S>::R, StageTw<L, S>::NS>(tid + b * Plan<L>::T, tw);
+    st.t[b] = load_tw<L, StageTw<L, S>::R, StageTw<L, S>::NS, TW>(tid + b * Plan<L>::T, tw);
   return st;
 }
 template <int L, int S, int DIR>
@@ -245,10 +271,9 @@ __device__ __forceinline__ void stage_regs(double2 (&v)[16], const StageTw<L, S>
 #pragma unroll
   for (int b = 0; b < 16 / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);
 }
-template <int L, int S, int DIR>
-__device__ __forceinline__ void stage_regs(double2 (&v)[16], int tid,
-                                           const double2* __restrict__ tw) {
-  stage_regs<L, S, DIR>(v, stage_tw<L, S>(tid, tw));
+template <int L, int S, int DIR, class TW>
+__device__ __forceinline__ void stage_regs(double2 (&v)[16], int tid, const TW& tw) {
+  stage_regs<L, S, DIR>(v, stage_tw<L, S, TW>(tid, tw));
 }
 
 // Stage input / output positions.
@@ -289,12 +314,12 @@ __device__ __forceinline__ void lds_read(const double2* buf, double2 (&v)[16], i
 
 // Middle stages S0..NSTAGES-1 (each: read LDS, barrier, compute, write LDS, barrier).
 // The caller has written stage S0-1's output to LDS and synchronised.
-template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1>
+template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW>
 __device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[16], int tid,
-                                           const double2* __restrict__ tw) {
+                                           const TW& tw) {
   using P = Plan<L>;
   if constexpr (S < P::NSTAGES) {
-    const StageTw<L, S> st = stage_tw<L, S>(tid, tw);
+    const StageTw<L, S> st = stage_tw<L, S, TW>(tid, tw);
     lds_read<L, S, IL>(buf, v, tid);
     __syncthreads();
     stage_regs<L, S, DIR>(v, st);
@@ -302,73 +327,131 @@ __device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[16], int t
       lds_write<L, S, IL>(buf, v, tid);
       __syncthreads();
     }
-    run_stages<L, S + 1, DIR, LAST_TO_LDS, IL>(buf, v, tid, tw);
+    run_stages<L, S + 1, DIR, LAST_TO_LDS, IL, TW>(buf, v, tid, tw);
   }
 }
 
+// Persistent work split: `nb` resident workgroups (a multiple of 8) process items [0, n).
+// XCD x = b % 8 owns the contiguous item range [x n/8, (x+1) n/8); its S = nb/8 workgroups
+// take that range with stride S, so at any moment an XCD works on S adjacent items (which
+// share 128-B lines) -- speed only, any placement is correct.
+struct Range {
+  int first, stride, count;
+};
+__device__ __forceinline__ Range persistent_range(int b, int nb, int n) {
+  Range r;
+  if ((nb & 7) == 0 && (n & 7) == 0 && nb <= n) {
+    const int S = nb >> 3, x = b & 7, s = b >> 3, per = n >> 3;
+    r.first = x * per + s;
+    r.stride = S;
+    r.count = s < per ? (per - s + S - 1) / S : 0;
+  } else {
+    r.first = b;
+    r.stride = nb;
+    r.count = b < n ? (n - b + nb - 1) / nb : 0;
+  }
+  return r;
+}
+
 // ---------------------------------------------------------------------------------------
-// Pass 1: rows, real -> packed half spectrum, column-tiled output.
+// Pass 1: rows, real -> packed half spectrum, column-major output H[m][y].
 // ---------------------------------------------------------------------------------------
 template <int L>
 struct RowCfg {
   static constexpr int T = Plan<L>::T;
-  static constexpr int XR = (256 / T) > 4 ? (256 / T) : 4;  // rows per workgroup
+  static constexpr int XR = (256 / T) > 4 ? (256 / T) : 4;  // rows per work item
   static constexpr int THREADS = XR * T;
+  static constexpr int PAIRS = (L / 2) * XR / THREADS;  // (m, L-m) pairs per thread
 };
+
+// Element pair p of a work item: row qq, columns m and L-m (m = p in [0, L/2)).  Lanes take
+// 16 consecutive m of one row, so both LDS accesses are contiguous per row and both global
+// accesses cover whole XR*16-B column segments.
+template <int L>
+__device__ __forceinline__ void pair_index(int e, int& qq, int& m) {
+  using C = RowCfg<L>;
+  qq = (e >> 4) % C::XR;
+  m = ((e >> 4) / C::XR) * 16 + (e & 15);
+}
+
+// Prefetch loads use a wave-uniform base pointer and unsigned 32-bit element offsets, so
+// each load needs one offset VGPR (global_load ... saddr) instead of a 64-bit address pair.
+template <int L>
+__device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __restrict__ f,
+                                           int y, int tid) {
+  // y is wave-uniform only when a row spans whole wavefronts (T >= 64)
+  const int yu = Plan<L>::T >= 64 ? __builtin_amdgcn_readfirstlane(y) : y;
+  const double2* z = reinterpret_cast<const double2*>(f) + (size_t)yu * L;
+  constexpr int R0 = Plan<L>::radix(0);
+#pragma unroll
+  for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+    for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[(unsigned)in_pos<L, 0>(tid, b, r)];
+}
 
 template <int L>
 __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
-    const double2* __restrict__ twL, const double2* __restrict__ twN) {
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
   using P = Plan<L>;
   using C = RowCfg<L>;
   __shared__ double2 lds[C::XR * P::ROWSTRIDE];
+  __shared__ TwLds<L> twL;      // W_L (row FFT stages)
+  __shared__ TwLds<2 * L> twN;  // W_N (r2c post-processing)
   const int q = threadIdx.x / P::T;
   const int tid = threadIdx.x % P::T;
-  const int y0 = blockIdx.x * C::XR;
   double2* buf = lds + q * P::ROWSTRIDE;
+  const Range rg = persistent_range(blockIdx.x, gridDim.x, M / C::XR);
 
-  // stage 0 straight from HBM: z[n] = f[2n] + i f[2n+1]
-  const double2* z = reinterpret_cast<const double2*>(f + (size_t)(y0 + q) * (2 * L));
-  double2 v[16];
-  constexpr int R0 = P::radix(0);
-#pragma unroll
-  for (int b = 0; b < 16 / R0; ++b)
-#pragma unroll
-    for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[in_pos<L, 0>(tid, b, r)];
-  stage_regs<L, 0, -1>(v, tid, twL);
-  lds_write<L, 0>(buf, v, tid);
+  // register double buffer: stage 0 runs on the prefetched rows in place; once its output
+  // is in LDS the registers are refilled with the next item while stages 1.. run.  The
+  // first item's loads are issued right behind the (older) twiddle-table loads, so the
+  // table fill's wait does not serialise them.
+  twL.fill(twL_);
+  twN.fill(twN_);
+  double2 nxt[16];
+  if (rg.count > 0) load_row_z<L>(nxt, f, rg.first * C::XR + q, tid);
   __syncthreads();
-  run_stages<L, 1, -1, true>(buf, v, tid, twL);
+  for (int it = 0; it < rg.count; ++it) {
+    const int y0 = (rg.first + it * rg.stride) * C::XR;
+    stage_regs<L, 0, -1>(nxt, tid, twL);
+    lds_write<L, 0>(buf, nxt, tid);
+    if (it + 1 < rg.count) load_row_z<L>(nxt, f, y0 + rg.stride * C::XR + q, tid);
+    __syncthreads();
+    double2 v[16];
+    run_stages<L, 1, -1, true>(buf, v, tid, twL);
 
-  // post-process: X[m] = E[m] + W_N^m O[m]; slot 0 = X[0] + i X[L].  Thread <-> element
-  // assignment chosen so consecutive lanes write consecutive addresses of a tile.
-  constexpr int PER = (L * C::XR) / C::THREADS;  // = 16
-#pragma unroll 4
-  for (int i = 0; i < PER; ++i) {
-    const int e = threadIdx.x + i * C::THREADS;
-    const int c = e & 1;
-    const int qq = (e >> 1) % C::XR;
-    const int t = (e >> 1) / C::XR;
-    const int m = 2 * t + c;
-    const double2* bq = lds + qq * P::ROWSTRIDE;
-    const double2 Zm = bq[padx(m)];
-    double2 X;
-    if (m == 0) {
-      X = make_double2(Zm.x + Zm.y, Zm.x - Zm.y);
-    } else {
-      const double2 Zc = cconj(bq[padx(L - m)]);
-      const double2 E = make_double2(0.5 * (Zm.x + Zc.x), 0.5 * (Zm.y + Zc.y));
-      const double2 D = csub(Zm, Zc);                       // = 2i O
-      const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
-      X = cadd(E, cmul(twN[m], O));
+    // post-process, two outputs per pair: X[m] = E[m] + W^m O[m], X[L-m] likewise;
+    // slot 0 = X[0] + i X[L]; m = L/2 is its own partner.
+#pragma unroll 1
+    for (int i = 0; i < C::PAIRS; ++i) {
+      int qq, m;
+      pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+      const double2* bq = lds + qq * P::ROWSTRIDE;
+      const double2 Zm = bq[padx(m)];
+      double2* Hrow = H + y0 + qq;
+      if (m == 0) {
+        Hrow[0] = make_double2(Zm.x + Zm.y, Zm.x - Zm.y);
+        const double2 Zh = bq[padx(L / 2)];  // X[L/2] = E + W^{L/2} O, W^{L/2} = -i
+        Hrow[(size_t)(L / 2) * M] = make_double2(Zh.x, -Zh.y);
+      } else {
+        const double2 Zp = bq[padx(L - m)];
+        const double2 Zc = cconj(Zp);
+        const double2 E = make_double2(0.5 * (Zm.x + Zc.x), 0.5 * (Zm.y + Zc.y));
+        const double2 D = csub(Zm, Zc);                       // = 2i O[m]
+        const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
+        const double2 WO = cmul(twN.w(m), O);
+        Hrow[(size_t)m * M] = cadd(E, WO);
+        // X[L-m] = conj(E[m]) + W^{L-m} conj(O[m]) = conj(E[m] - W^m O[m])
+        Hrow[(size_t)(L - m) * M] = cconj(csub(E, WO));
+      }
     }
-    H[((size_t)t * M + y0 + qq) * 2 + c] = X;
+    __syncthreads();  // LDS is rewritten by the next item
   }
 }
 
 // ---------------------------------------------------------------------------------------
-// Pass 2: columns of one 2-column tile: forward FFT, divide, inverse FFT, in place.
+// Pass 2: one column at a time: forward FFT, divide, inverse FFT, in place.
 // ---------------------------------------------------------------------------------------
 struct DivArgs {
   const double* cx;  // cos(kx[m]), m <= L
@@ -378,124 +461,188 @@ struct DivArgs {
   int neg;
 };
 
+// After the forward transform's last stage a thread holds elements (j_b + r*NS), the same
+// set the inverse transform's stage 0 reads (tid + T*r'), in a different register order:
+// r' = b + (16/R_last)*r.  fwd_to_inv permutes the registers accordingly.
 template <int M>
-__global__ __launch_bounds__(2 * Plan<M>::T) void cols_kernel(double2* __restrict__ H,
-                                                            const double2* __restrict__ twM,
-                                                            const DivArgs da) {
+__device__ __forceinline__ void fwd_to_inv(const double2 (&a)[16], double2 (&v)[16]) {
   using P = Plan<M>;
-  __shared__ double2 lds[2 * P::PAD];
-  const int c = threadIdx.x & 1;
-  const int tid = threadIdx.x >> 1;
-  const int t = blockIdx.x;
-  double2* buf = lds + c;                      // interleaved columns: buf[2*padx(p)]
-  double2* tile = H + (size_t)t * M * 2 + c;  // element y at tile[2*y]
+  constexpr int RL = P::radix(P::NSTAGES - 1);
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) v[b + (16 / RL) * r] = a[b * RL + r];
+}
+
+template <int M>
+__device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __restrict__ col,
+                                         int tid) {
+  constexpr int R0 = Plan<M>::radix(0);
+#pragma unroll
+  for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+    for (int r = 0; r < R0; ++r) a[b * R0 + r] = col[(unsigned)in_pos<M, 0>(tid, b, r)];
+}
+
+template <int M>
+__global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ H,
+                                                        const double2* __restrict__ twM_,
+                                                        const DivArgs da) {
+  // One column per workgroup (2 resident per CU): not persistent, because the divide's
+  // cy[k] loads would queue behind a next-column prefetch (vmcnt is in order).
+  using P = Plan<M>;
+  static_assert(P::NSTAGES >= 2, "column length");
+  __shared__ double2 lds[P::PAD];
+  const TwGlobal<M> twM{twM_};
+  const int tid = threadIdx.x;
+  const int m = xcd_remap(blockIdx.x, gridDim.x);
+  const double sgn = da.neg ? -1.0 : 1.0;
+  double2* col = H + (size_t)m * M;
+
+  double2 a[16];
+  load_col<M>(a, col, tid);
+  stage_regs<M, 0, -1>(a, tid, twM);
+  lds_write<M, 0>(lds, a, tid);
+  __syncthreads();
+  run_stages<M, 1, -1, false>(lds, a, tid, twM);  // last stage stays in registers
 
   double2 v[16];
-  constexpr int R0 = P::radix(0);
-#pragma unroll
-  for (int b = 0; b < 16 / R0; ++b)
-#pragma unroll
-    for (int r = 0; r < R0; ++r) v[b * R0 + r] = tile[2 * in_pos<M, 0>(tid, b, r)];
-  stage_regs<M, 0, -1>(v, tid, twM);
-  lds_write<M, 0, 2>(buf, v, tid);
-  __syncthreads();
-  run_stages<M, 1, -1, true, 2>(buf, v, tid, twM);  // natural-order spectrum in LDS
-
-  // divide (Common.jl:118-121) fused into the first inverse stage's loads
-  const int m = 2 * t + c;
-  const double sgn = da.neg ? -1.0 : 1.0;
+  fwd_to_inv<M>(a, v);  // v[r] = spectrum at k = tid + T*r, natural order
   const double ax = fd_symbol_x(da.aa, da.bb, da.cx[m]);
-  const double axL = fd_symbol_x(da.aa, da.bb, da.cx[da.L]);
+  if (m != 0) {
 #pragma unroll
-  for (int b = 0; b < 16 / R0; ++b)
-#pragma unroll
-    for (int r = 0; r < R0; ++r) {
-      const int k = in_pos<M, 0>(tid, b, r);
-      const double2 Z = buf[2 * padx(k)];
-      const double cyk = da.cy[k];
-      double2 o;
-      if (m != 0) {
-        const double d = fd_symbol(ax, da.cc, cyk);
-        o = make_double2((sgn * Z.x / d) * da.scale, (sgn * Z.y / d) * da.scale);
-      } else {
-        // packed column: Z = FFT_y(X_dc + i X_nyq); split, divide each, re-pack
-        const double2 Zc = cconj(buf[2 * padx((M - k) & (M - 1))]);
-        const double2 A = make_double2(0.5 * (Z.x + Zc.x), 0.5 * (Z.y + Zc.y));
-        const double2 D = csub(Z, Zc);
-        const double2 B = make_double2(0.5 * D.y, -0.5 * D.x);
-        const double d0 = fd_symbol(ax, da.cc, cyk);   // kx = eps column
-        const double dL = fd_symbol(axL, da.cc, cyk);  // kx = -pi column
-        const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0
-                                  : make_double2(sgn * A.x / d0, sgn * A.y / d0);
-        const double2 B2 = make_double2(sgn * B.x / dL, sgn * B.y / dL);
-        o = make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
-      }
-      v[b * R0 + r] = o;
+    for (int r = 0; r < 16; ++r) {
+      const int k = tid + P::T * r;
+      const double d = fd_symbol(ax, da.cc, da.cy[k]);
+      v[r] = make_double2((sgn * v[r].x / d) * da.scale, (sgn * v[r].y / d) * da.scale);
     }
-  __syncthreads();
-  stage_regs<M, 0, 1>(v, tid, twM);
-  if constexpr (P::NSTAGES > 1) {
-    lds_write<M, 0, 2>(buf, v, tid);
+  } else {
+    // packed column: Z = FFT_y(X_dc + i X_nyq); split with Z[-k], divide each half by its
+    // own symbol (kx = eps and kx = -pi), re-pack.  Partners come through LDS.
+    __syncthreads();  // all reads of the last forward stage are done
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lds[padx(tid + P::T * r)] = v[r];
     __syncthreads();
-    run_stages<M, 1, 1, false, 2>(buf, v, tid, twM);
+    const double axL = fd_symbol_x(da.aa, da.bb, da.cx[da.L]);
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = tid + P::T * r;
+      const double2 Z = v[r];
+      const double2 Zc = cconj(lds[padx((M - k) & (M - 1))]);
+      const double2 A = make_double2(0.5 * (Z.x + Zc.x), 0.5 * (Z.y + Zc.y));
+      const double2 D = csub(Z, Zc);
+      const double2 B = make_double2(0.5 * D.y, -0.5 * D.x);
+      const double cyk = da.cy[k];
+      const double d0 = fd_symbol(ax, da.cc, cyk);   // kx = eps column
+      const double dL = fd_symbol(axL, da.cc, cyk);  // kx = -pi column
+      const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0 (Common.jl:118)
+                                : make_double2(sgn * A.x / d0, sgn * A.y / d0);
+      const double2 B2 = make_double2(sgn * B.x / dL, sgn * B.y / dL);
+      v[r] = make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
+    }
   }
+  __syncthreads();  // LDS is rewritten by the inverse stage 0
+  stage_regs<M, 0, 1>(v, tid, twM);
+  lds_write<M, 0>(lds, v, tid);
+  __syncthreads();
+  run_stages<M, 1, 1, false>(lds, v, tid, twM);
   // last inverse stage: outputs j + r*NS are in natural order -> straight to HBM
   constexpr int SL = P::NSTAGES - 1;
   constexpr int RL = P::radix(SL);
 #pragma unroll
   for (int b = 0; b < 16 / RL; ++b)
 #pragma unroll
-    for (int r = 0; r < RL; ++r) tile[2 * out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
+    for (int r = 0; r < RL; ++r) col[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
 }
 
 // ---------------------------------------------------------------------------------------
 // Pass 3: rows, packed half spectrum -> real (c2r).
 // ---------------------------------------------------------------------------------------
+// One pair (m, L-m) per slot: Z[m] = (X[m] + conj X[L-m]) + i W_N^{-m} (X[m] - conj X[L-m]),
+// Z[L-m] = conj of the same expression with m and L-m swapped.
+template <int L>
+struct InvLoads {
+  double2 xm[RowCfg<L>::PAIRS], xp[RowCfg<L>::PAIRS];
+  double2 xh;  // X[L/2] for the thread that owns m = 0
+};
+template <int L>
+__device__ __forceinline__ void load_inv(InvLoads<L>& ld, const double2* __restrict__ H, int M,
+                                         int y0) {
+  using C = RowCfg<L>;
+  const double2* base = H + __builtin_amdgcn_readfirstlane(y0);
+#pragma unroll
+  for (int i = 0; i < C::PAIRS; ++i) {
+    int qq, m;
+    pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+    ld.xm[i] = base[(unsigned)(m * M + qq)];
+    ld.xp[i] = base[(unsigned)(((L - m) & (L - 1)) * M + qq)];  // m = 0: unused
+    if (m == 0) ld.xh = base[(unsigned)((L / 2) * M + qq)];
+  }
+}
+
 template <int L>
 __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_inv_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
-    const double2* __restrict__ twL, const double2* __restrict__ twN) {
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
   using P = Plan<L>;
   using C = RowCfg<L>;
   __shared__ double2 lds[C::XR * P::ROWSTRIDE];
-  const int y0 = blockIdx.x * C::XR;
-
-  // pre-process: Z[m] = (X[m] + conj X[L-m]) + i W_N^{-m} (X[m] - conj X[L-m])
-  constexpr int PER = (L * C::XR) / C::THREADS;
-#pragma unroll 4
-  for (int i = 0; i < PER; ++i) {
-    const int e = threadIdx.x + i * C::THREADS;
-    const int c = e & 1;
-    const int qq = (e >> 1) % C::XR;
-    const int t = (e >> 1) / C::XR;
-    const int m = 2 * t + c;
-    const double2 Xm = H[((size_t)t * M + y0 + qq) * 2 + c];
-    double2 Z;
-    if (m == 0) {  // slot 0 = (X[0], X[L]), both real
-      Z = make_double2(Xm.x + Xm.y, Xm.x - Xm.y);
-    } else {
-      const int mp = L - m;
-      const double2 Xp = cconj(H[((size_t)(mp >> 1) * M + y0 + qq) * 2 + (mp & 1)]);
-      const double2 S = cadd(Xm, Xp);
-      const double2 D = cmul(cconj(twN[m]), csub(Xm, Xp));
-      Z = make_double2(S.x - D.y, S.y + D.x);
-    }
-    lds[qq * P::ROWSTRIDE + padx(m)] = Z;
-  }
-  __syncthreads();
-
+  __shared__ TwLds<L> twL;
+  __shared__ TwLds<2 * L> twN;
   const int q = threadIdx.x / P::T;
   const int tid = threadIdx.x % P::T;
   double2* buf = lds + q * P::ROWSTRIDE;
-  double2 v[16];
-  run_stages<L, 0, 1, false>(buf, v, tid, twL);
-  constexpr int SL = P::NSTAGES - 1;
-  constexpr int RL = P::radix(SL);
-  double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + q) * (2 * L));
+  const Range rg = persistent_range(blockIdx.x, gridDim.x, M / C::XR);
+
+  // register double buffer: the prefetched spectrum pairs are consumed into LDS, then the
+  // registers are refilled with the next item while the FFT runs.
+  twL.fill(twL_);
+  twN.fill(twN_);
+  InvLoads<L> nxt;
+  if (rg.count > 0) load_inv<L>(nxt, H, M, rg.first * C::XR);
+  __syncthreads();
+  for (int it = 0; it < rg.count; ++it) {
+    const int y0 = (rg.first + it * rg.stride) * C::XR;
 #pragma unroll
-  for (int b = 0; b < 16 / RL; ++b)
+    for (int i = 0; i < C::PAIRS; ++i) {
+      int qq, m;
+      pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+      double2* bq = lds + qq * P::ROWSTRIDE;
+      const double2 Xm = nxt.xm[i];
+      if (m == 0) {  // slot 0 = (X[0], X[L]), both real; Z[L/2] = 2 conj(X[L/2])
+        bq[padx(0)] = make_double2(Xm.x + Xm.y, Xm.x - Xm.y);
+        bq[padx(L / 2)] = make_double2(2.0 * nxt.xh.x, -2.0 * nxt.xh.y);
+      } else {
+        const double2 Xp = cconj(nxt.xp[i]);  // conj X[L-m]
+        const double2 S = cadd(Xm, Xp);
+        const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
+        bq[padx(m)] = make_double2(S.x - D.y, S.y + D.x);
+        // Z[L-m] = S' + i D' with S' = conj(S), D' = W^{-(L-m)} (X[L-m] - conj X[m]) = conj(D)
+        bq[padx(L - m)] = make_double2(S.x + D.y, D.x - S.y);
+      }
+    }
+    if (it + 1 < rg.count) load_inv<L>(nxt, H, M, y0 + rg.stride * C::XR);
+    __syncthreads();
+
+    double2 v[16];
+    run_stages<L, 0, 1, false>(buf, v, tid, twL);
+    constexpr int SL = P::NSTAGES - 1;
+    constexpr int RL = P::radix(SL);
+    double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + q) * (2 * L));
 #pragma unroll
-    for (int r = 0; r < RL; ++r) z[out_pos<L, SL>(tid, b, r)] = v[b * RL + r];
+    for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+      for (int r = 0; r < RL; ++r) z[out_pos<L, SL>(tid, b, r)] = v[b * RL + r];
+    __syncthreads();  // LDS is rewritten by the next item
+  }
+}
+
+// Persistent grid: `per_cu` resident workgroups per CU (LDS-limited), a multiple of 8.
+static int persistent_grid(int ncu, int per_cu, int items) {
+  int nb = ncu * per_cu;
+  nb -= nb % 8;
+  if (nb < 8) nb = 8;
+  return nb < items ? nb : items;
 }
 
 template <int N>
@@ -503,16 +650,21 @@ void launch_fused_n(int pass, const FusedPoissonArgs& a, hipStream_t st) {
   constexpr int L = N / 2;
   using C = RowCfg<L>;
   const int M = N;
+  // LDS: rows kernels XR*(L+L/16)*16 B, cols (M+M/16)*16 B -> blocks per CU (160 KB)
+  constexpr int row_lds = C::XR * Plan<L>::ROWSTRIDE * 16 + sizeof(TwLds<L>) + sizeof(TwLds<N>);
+  constexpr int col_lds = Plan<N>::PAD * 16;
+  const int row_per_cu = (160 * 1024) / row_lds;
+  const int col_per_cu = (160 * 1024) / col_lds;
   if (pass == 0) {
-    hipLaunchKernelGGL(rows_fwd_kernel<L>, dim3(M / C::XR), dim3(C::THREADS), 0, st, a.f, a.H,
-                       M, a.twL, a.twN);
+    hipLaunchKernelGGL(rows_fwd_kernel<L>, dim3(persistent_grid(a.ncu, row_per_cu, M / C::XR)),
+                       dim3(C::THREADS), 0, st, a.f, a.H, M, a.twL, a.twN);
   } else if (pass == 1) {
     DivArgs da{a.cx, a.cy, a.aa, a.bb, a.cc, a.scale, L, a.neg ? 1 : 0};
-    hipLaunchKernelGGL(cols_kernel<N>, dim3(L / 2), dim3(2 * Plan<N>::T), 0, st, a.H, a.twN,
-                       da);
+    (void)col_per_cu;
+    hipLaunchKernelGGL(cols_kernel<N>, dim3(L), dim3(Plan<N>::T), 0, st, a.H, a.twN, da);
   } else {
-    hipLaunchKernelGGL(rows_inv_kernel<L>, dim3(M / C::XR), dim3(C::THREADS), 0, st, a.H, a.s,
-                       M, a.twL, a.twN);
+    hipLaunchKernelGGL(rows_inv_kernel<L>, dim3(persistent_grid(a.ncu, row_per_cu, M / C::XR)),
+                       dim3(C::THREADS), 0, st, a.H, a.s, M, a.twL, a.twN);
   }
   CFDJ_HIP(hipGetLastError());
 }

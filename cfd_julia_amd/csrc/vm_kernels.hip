@@ -94,7 +94,12 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nx = p.nx, ny = p.ny;
-  const int x = blockIdx.x * kColsPerWave + 2 * lane;
+  // 1-D grid, XCD-aware: each XCD sweeps a contiguous band of (strip, chunk) tiles, strips
+  // fastest, so x-neighbour strips and adjacent row chunks share one L2.
+  const int strips = (nx + kColsPerWave - 1) / kColsPerWave;
+  const int tile = xcd_remap(blockIdx.x, gridDim.x);
+  const int strip = tile % strips, chunk = tile / strips;
+  const int x = strip * kColsPerWave + 2 * lane;
   const bool valid = x < nx;
   const int xs = valid ? x : 0;
   const bool is_l = lane == 0;
@@ -102,7 +107,7 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
   const int xl = xs == 0 ? nx - 1 : xs - 1;
   const int xr = xs + 2 >= nx ? xs + 2 - nx : xs + 2;
 
-  const int ybeg = (blockIdx.y * kWavesPerBlock + wave) * p.rows_per_wave;
+  const int ybeg = (chunk * kWavesPerBlock + wave) * p.rows_per_wave;
   if (ybeg >= ny) return;
   const int yend = min(ybeg + p.rows_per_wave, ny);
 
@@ -207,8 +212,10 @@ __global__ __launch_bounds__(256) void finite_kernel(const double* __restrict__ 
 
 void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   const int rpw = p.rows_per_wave;
-  dim3 grid((p.nx + kColsPerWave - 1) / kColsPerWave,
-            (p.ny + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw));
+  const long strips = (p.nx + kColsPerWave - 1) / kColsPerWave;
+  const long chunks = (p.ny + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw);
+  if (strips * chunks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
+  dim3 grid((unsigned)(strips * chunks));
   dim3 block(kWave * kWavesPerBlock);
   switch (stage) {
     case 0: hipLaunchKernelGGL(vm_stage_kernel<0>, grid, block, 0, st, p); break;
