@@ -47,6 +47,20 @@ def stable_dt(nx):
     return 5e-4 * (4096.0 / nx) ** 2
 
 
+def load_pmc(nx):
+    """PMC traffic of the stage kernel from the committed rocprofv3 summary
+    (tools/pmc_summary.py output, separate --pmc passes, FETCH_SIZE doubled for gfx950)."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("nx") != nx:
+        return None
+    return d
+
+
 def cpu_baseline(nx, steps, workers):
     """The CPU oracle (NumPy + scipy.fft restatement of vm.jl/Common.jl) on this host."""
     from oracle import vm_oracle as vo
@@ -130,22 +144,37 @@ def main():
     h.upload(wn)
     del wn
 
+    def timed(instrumented):
+        """One timed region of exactly K steps, barrier + device sync on both sides."""
+        h.set_timing(instrumented)
+        barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        h.step_async(dt, args.steps)
+        h.sync()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        kern = h.timing() if instrumented else None
+        h.set_timing(False)
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt[0])
+        return el, kern
+
+    # warm-up: also captures the HIP graph of K steps that the headline region replays
     h.step(dt, args.warmup)
-    h.set_timing(not args.no_timing)
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
     h.step_async(dt, args.steps)
     h.sync()
-    torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
-    kern = h.timing()
-    h.set_timing(False)
-    if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt[0])
+    # (1) headline: graph replay (single-GPU fused path), no instrumentation
+    elapsed, _ = timed(False)
+    # (2) the same K steps again with HIP events around every kernel on the handle's
+    # stream (eager launches: event nodes cannot be captured into graphs on this ROCm)
+    if args.no_timing:
+        elapsed_i, kern = None, {k: (0.0, 0) for k in _lib.K_NAMES}
+    else:
+        elapsed_i, kern = timed(True)
 
     # sanity: the state stays finite and bounded (conservative scheme)
     h.set_check_finite(True)
@@ -169,7 +198,13 @@ def main():
         "alg_bytes_per_launch": int(round(stage_alg_bytes / max(stage_n, 1))),
         "avg_launch_us": round(stage_ms * 1e3 / max(stage_n, 1), 2),
         "launches": stage_n,
+        "source": "HIP events around every kernel on the handle stream, over a second "
+                  "timed region of the same K steps (eager launches)",
     }
+    pmc = load_pmc(nx)
+    if pmc:
+        roofline["traffic"] = pmc["stage_bytes_per_launch"]
+        roofline["traffic_source"] = pmc["source"]
     step_gbs = STEP_BYTES_PER_CELL * local_cells * args.steps / elapsed / 1e9
     breakdown = {k: {"ms_per_step": round(v[0] / max(args.steps, 1), 4), "launches": v[1]}
                  for k, v in kern.items() if v[1]}
@@ -190,6 +225,7 @@ def main():
         "config": {"workload": f"NS2D vortex merger {nx}x{ny} periodic, Arakawa + FD-FFT "
                                f"Poisson + SSP-RK3 (vm.jl)", "nx": nx, "ny": ny, "dt": dt,
                    "re": re, "parallelism": "single" if n_gpus == 1 else f"yslab{n_gpus}"},
+        "ms_per_step_instrumented": round(elapsed_i * 1e3 / args.steps, 4) if elapsed_i else None,
         "achieved_hbm_gbs_step": round(step_gbs, 1),
         "step_roofline_frac": round(step_gbs / HBM_PEAK_GBS, 4),
         "kernels": breakdown,

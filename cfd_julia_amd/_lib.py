@@ -72,6 +72,7 @@ SIGNATURES = {
     "cfdj_vm_field_device": (C.c_int, [_vp, C.POINTER(_vp)]),
     "cfdj_vm_slab": (C.c_int, [_vp, _ip, _ip]),
     "cfdj_vm_set_rows_per_wave": (C.c_int, [_vp, C.c_int]),
+    "cfdj_vm_set_graph": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_get_poisson": (C.c_int, [_vp]),
     "cfdj_fps_set_poisson": (C.c_int, [_vp, C.c_int]),

@@ -335,19 +335,26 @@ struct cfdj_vm {
   // finiteness check
   bool check_finite = false;
   int* d_flag = nullptr;
+  // HIP graph of `nsteps` whole RK3 steps (single-GPU fused-Poisson handles), re-captured
+  // when dt / nsteps / tuning change.
+  bool use_graph = true;
+  hipGraphExec_t gexec = nullptr;
+  double g_dt = 0.0;
+  int g_steps = -1;
 
   bool slab_mode() const { return mode != Mode::Single; }
 
   // ---- timing -----------------------------------------------------------------------
+  void reserve_events(size_t n) {
+    while (ev.size() < n) {
+      hipEvent_t e;
+      CFDJ_HIP(hipEventCreate(&e));
+      ev.push_back(e);
+    }
+  }
   void tbegin(int cat) {
     if (!timing) return;
-    if (ev_used + 2 > ev.size()) {
-      for (int i = 0; i < 64; ++i) {
-        hipEvent_t e;
-        CFDJ_HIP(hipEventCreate(&e));
-        ev.push_back(e);
-      }
-    }
+    if (ev_used + 2 > ev.size()) reserve_events(ev.size() + 64);
     CFDJ_HIP(hipEventRecord(ev[ev_used], stream));
     ev_cat.push_back(cat);
   }
@@ -538,12 +545,48 @@ struct cfdj_vm {
     }
   }
 
-  void step_async(double dt, int nsteps) {
+  void steps_eager(double dt, int nsteps) {
     for (int n = 0; n < nsteps; ++n) {
       stage(1, dt);
       stage(2, dt);
       stage(3, dt);
     }
+  }
+
+  void invalidate_graph() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    gexec = nullptr;
+    g_steps = -1;
+  }
+
+  void step_async(double dt, int nsteps) {
+    if (nsteps == 0) return;
+    // Graphs only around our own kernels (rocFFT calls are not captured), and never with
+    // timing on: event-record nodes captured from hipEventRecord are not recorded on this
+    // ROCm (hipEventElapsedTime -> invalid resource handle), so timed runs launch eagerly.
+    if (!use_graph || timing || mode != Mode::Single || !use_fused) {
+      steps_eager(dt, nsteps);
+      return;
+    }
+    if (!gexec || g_dt != dt || g_steps != nsteps) {
+      invalidate_graph();
+      hipGraph_t g = nullptr;
+      CFDJ_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      try {
+        steps_eager(dt, nsteps);
+      } catch (...) {
+        (void)hipStreamEndCapture(stream, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+      }
+      CFDJ_HIP(hipStreamEndCapture(stream, &g));
+      const hipError_t e = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      CFDJ_HIP(e);
+      g_dt = dt;
+      g_steps = nsteps;
+    }
+    CFDJ_HIP(hipGraphLaunch(gexec, stream));
   }
 
   void sync() {
@@ -614,6 +657,7 @@ struct cfdj_vm {
 
   ~cfdj_vm() {
     if (stream) (void)hipStreamSynchronize(stream);
+    invalidate_graph();
     for (auto& s : slabs) s.destroy();
     plans.destroy();
     sym.destroy();
@@ -958,6 +1002,7 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
     CFDJ_REQUIRE(rows >= 1, "rows must be >= 1");
     h->rows_per_wave = rows;
+    h->invalidate_graph();
   });
 }
 
@@ -969,6 +1014,17 @@ int cfdj_vm_set_poisson(cfdj_vm* h, int path) {
     const bool f = resolve_fused(path, h->nx, h->ny, h->slab_mode());
     if (f && !h->fused.twN) h->fused.init(h->nx);
     h->use_fused = f;
+    h->invalidate_graph();
+  });
+}
+
+int cfdj_vm_set_graph(cfdj_vm* h, int enable) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    select_device(h->device);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    h->use_graph = enable != 0;
+    h->invalidate_graph();
   });
 }
 

@@ -154,6 +154,9 @@ class VortexMerger:
         check(_lib.load().cfdj_vm_set_rows_per_wave(self._h, int(rows)),
               "cfdj_vm_set_rows_per_wave")
 
+    def set_graph(self, enable=True):
+        check(_lib.load().cfdj_vm_set_graph(self._h, int(bool(enable))), "cfdj_vm_set_graph")
+
     def set_poisson(self, path):
         """path: "auto" | "rocfft" | "fused" (CFDJ_POISSON_*)."""
         check(_lib.load().cfdj_vm_set_poisson(self._h, _PATHS[path]), "cfdj_vm_set_poisson")

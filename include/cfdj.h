@@ -126,6 +126,9 @@ int cfdj_vm_field_device(cfdj_vm* h, double** w_dev);
 int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows);
 /* Tuning: rows marched by one wavefront in the stage kernel (default chosen per size). */
 int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
+/* Replay cfdj_vm_step's kernel sequence from a captured HIP graph (default on; used on
+ * single-GPU handles with the fused Poisson path, others launch eagerly). */
+int cfdj_vm_set_graph(cfdj_vm* h, int enable);
 /* Select / query the Poisson implementation (CFDJ_POISSON_*; single-GPU handles). */
 int cfdj_vm_set_poisson(cfdj_vm* h, int path);
 int cfdj_vm_get_poisson(cfdj_vm* h);

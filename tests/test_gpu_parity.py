@@ -314,3 +314,25 @@ def test_gpu_poisson_path_selection(cfdj):
             h.set_poisson("fused")
     with cfdj.VortexMerger(1024, 1024, dx, dy, 1000.0, kind="virtual", nranks=2) as h:
         assert h.poisson() == "rocfft"
+
+
+def test_gpu_graph_timing_many_steps(cfdj):
+    """Graph replay (untimed) and eager timed launches give identical fields; timing over
+    many steps harvests every kernel."""
+    n = 1024
+    dx, dy, w0 = vm_setup(n)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.upload_interior(w0)
+        h.step(0.008, 3)
+        h.set_timing(True)
+        h.step_async(0.008, 50)
+        h.sync()
+        t = h.timing()
+        h.set_timing(False)
+        w_graph = h.download_interior()
+        h.set_graph(False)
+        h.upload_interior(w0)
+        h.step(0.008, 53)
+        w_eager = h.download_interior()
+    assert t["stage"][1] == 150 and t["fft_fwd"][1] == 150 and t["fft_inv"][1] == 150
+    assert np.array_equal(w_graph, w_eager)
