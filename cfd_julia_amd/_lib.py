@@ -22,6 +22,7 @@ ERR_NAMES = {-1: "CFDJ_ERR_ARG", -2: "CFDJ_ERR_HIP", -3: "CFDJ_ERR_ROCFFT",
 K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
 POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED = 0, 1, 2
+SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1
 
 
 class CfdjError(RuntimeError):
@@ -76,6 +77,7 @@ SIGNATURES = {
     "cfdj_vm_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_get_poisson": (C.c_int, [_vp]),
     "cfdj_fps_set_poisson": (C.c_int, [_vp, C.c_int]),
+    "cfdj_fps_set_symbol": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_destroy": (None, [_vp]),
 }
 

@@ -15,6 +15,7 @@ namespace cfdj {
 
 // ---- errors ------------------------------------------------------------------------
 void set_error(const std::string& msg);
+const char* last_error();
 
 struct Error {
   int code;

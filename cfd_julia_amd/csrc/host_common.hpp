@@ -1,0 +1,264 @@
+// Host-side helpers shared by the libcfdj.so translation units: error guard, device
+// allocation, the Poisson symbol tables, rocFFT plan bundles and the fused-FFT state.
+#pragma once
+
+#include "cfdj_internal.hpp"
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <new>
+
+namespace cfdj {
+
+template <class F>
+inline int guard(F&& f) {
+  try {
+    f();
+    return CFDJ_OK;
+  } catch (const Error& e) {
+    set_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_error("host allocation failed");
+    return CFDJ_ERR_HIP;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return CFDJ_ERR_STATE;
+  } catch (...) {
+    set_error("unknown C++ exception");
+    return CFDJ_ERR_STATE;
+  }
+}
+
+inline void fft_setup() {
+  static std::once_flag once;
+  static rocfft_status st = rocfft_status_success;
+  std::call_once(once, [] { st = rocfft_setup(); });
+  CFDJ_FFT(st);
+}
+
+inline void select_device(int device) {
+  if (device >= 0) CFDJ_HIP(hipSetDevice(device));
+}
+
+template <class T>
+inline T* dalloc(size_t n) {
+  void* p = nullptr;
+  CFDJ_HIP(hipMalloc(&p, n * sizeof(T) + 16));
+  return static_cast<T*>(p);
+}
+
+template <class T>
+inline void dfree(T*& p) {
+  if (p) (void)hipFree((void*)p);
+  p = nullptr;
+}
+
+// Common.jl:106-113 wavenumber table (0-based): kx[0] = eps, kx[m] = hx*m for m < nx/2,
+// kx[m] = hx*(m - nx) for m >= nx/2, hx = 2pi/nx.
+inline std::vector<double> kx_table(int nx, double eps) {
+  std::vector<double> kx(nx);
+  const double hx = (2.0 * M_PI) / nx;
+  const int h = nx / 2;
+  for (int i = 1; i <= h; ++i) {
+    kx[i - 1] = hx * (double)(i - 1);
+    kx[i + h - 1] = hx * (double)(i - h - 1);
+  }
+  kx[0] = eps;
+  return kx;
+}
+
+inline void check_grid(int nx, int ny, double dx, double dy) {
+  CFDJ_REQUIRE(nx >= 4 && ny >= 4, "nx and ny must be >= 4");
+  CFDJ_REQUIRE(nx % 2 == 0, "nx must be even (Common.jl:108 loops to nx/2)");
+  CFDJ_REQUIRE(ny <= nx, "ny > nx: Common.jl:113 aliases ky = kx (BoundsError)");
+  CFDJ_REQUIRE(dx > 0 && dy > 0 && std::isfinite(dx) && std::isfinite(dy),
+               "dx, dy must be positive and finite");
+}
+
+// ---- spectral symbol tables + constants (Common.jl:101-103, 119-121) ----------------
+struct Symbol {
+  int nx = 0, ny = 0, nxh = 0, kind = CFDJ_SYMBOL_FD;
+  double aa = 0, bb = 0, cc = 0, scale = 0;
+  double* cx = nullptr;  // FD: cos(kx[m]); spectral: kx[m]^2   (m < nxh)
+  double* cy = nullptr;  // FD: cos(ky[n]); spectral: -ky[n]^2  (n < ny)
+  double* cy_mirror = nullptr;  // ny < nx: cy[(ny - n) % ny] (see DivideParams)
+  // The divide evaluates (aa + bb*cx[m]) + cc*cy[n] without FMA.
+  //  FD (Common.jl:101-103,119-121):  aa + bb cos kx + cc cos ky, kx = 2pi/nx * index.
+  //  spectral (fft_s.jl:18-34):       (-kx^2) - ky^2 = (0 + (-1)*kx^2) + 1*(-ky^2)
+  //    with kx = 2pi/(nx dx) * index -- every extra operation is exact, so the result is
+  //    bit-identical to the reference expression.
+  void init(int nx_, int ny_, double dx, double dy, double eps, int kind_ = CFDJ_SYMBOL_FD) {
+    nx = nx_;
+    ny = ny_;
+    nxh = nx / 2 + 1;
+    kind = kind_;
+    scale = 1.0 / ((double)nx * (double)ny);  // ifft normalisation, folded into divide
+    std::vector<double> hcx(nxh), hcy(ny);
+    if (kind == CFDJ_SYMBOL_FD) {
+      aa = -2.0 / (dx * dx) - 2.0 / (dy * dy);
+      bb = 2.0 / (dx * dx);
+      cc = 2.0 / (dy * dy);
+      std::vector<double> kx = kx_table(nx, eps);
+      for (int m = 0; m < nxh; ++m) hcx[m] = std::cos(kx[m]);
+      for (int n = 0; n < ny; ++n) hcy[n] = std::cos(kx[n]);
+    } else {
+      aa = 0.0;
+      bb = -1.0;
+      cc = 1.0;
+      // fft_s.jl:19-27: hx = 2pi/(nx dx); kx[i] = hx(i-1), kx[i+nx/2] = hx(i - nx/2 - 1.)
+      std::vector<double> kx(nx);
+      const double hx = (2.0 * M_PI) / ((double)nx * dx);
+      const int h = nx / 2;
+      for (int i = 1; i <= h; ++i) {
+        kx[i - 1] = hx * (double)(i - 1);
+        kx[i + h - 1] = hx * ((double)(i - h) - 1.0);
+      }
+      kx[0] = eps;
+      for (int m = 0; m < nxh; ++m) hcx[m] = kx[m] * kx[m];
+      for (int n = 0; n < ny; ++n) hcy[n] = -(kx[n] * kx[n]);
+    }
+    cx = dalloc<double>(nxh);
+    cy = dalloc<double>(ny);
+    CFDJ_HIP(hipMemcpy(cx, hcx.data(), nxh * sizeof(double), hipMemcpyHostToDevice));
+    CFDJ_HIP(hipMemcpy(cy, hcy.data(), ny * sizeof(double), hipMemcpyHostToDevice));
+    if (ny != nx) {
+      std::vector<double> hm(ny);
+      for (int n = 0; n < ny; ++n) hm[n] = hcy[(ny - n) % ny];
+      cy_mirror = dalloc<double>(ny);
+      CFDJ_HIP(hipMemcpy(cy_mirror, hm.data(), ny * sizeof(double), hipMemcpyHostToDevice));
+    }
+  }
+  void destroy() {
+    dfree(cx);
+    dfree(cy);
+    dfree(cy_mirror);
+  }
+  DivideParams divide(double2* spec, int width, int rows, int pitch, int kx_off,
+                      bool neg) const {
+    DivideParams p;
+    p.spec = spec;
+    p.cx = cx;
+    p.cy = cy;
+    p.cy_mirror = cy_mirror;
+    p.width = width;
+    p.rows = rows;
+    p.pitch = pitch;
+    p.kx_off = kx_off;
+    p.nxh = nxh;
+    p.aa = aa;
+    p.bb = bb;
+    p.cc = cc;
+    p.scale = scale;
+    p.neg = neg;
+    return p;
+  }
+};
+
+// ---- rocFFT plan bundle --------------------------------------------------------------
+struct Plans {
+  std::vector<rocfft_plan> plans;
+  rocfft_execution_info info = nullptr;
+  void* work = nullptr;
+  size_t work_bytes = 0;
+
+  rocfft_plan add(rocfft_transform_type type, rocfft_result_placement place, size_t dim,
+                  const size_t* lengths, size_t batch, rocfft_plan_description desc) {
+    rocfft_plan p = nullptr;
+    CFDJ_FFT(rocfft_plan_create(&p, place, type, rocfft_precision_double, dim, lengths, batch,
+                                desc));
+    plans.push_back(p);
+    size_t wb = 0;
+    CFDJ_FFT(rocfft_plan_get_work_buffer_size(p, &wb));
+    if (wb > work_bytes) work_bytes = wb;
+    return p;
+  }
+  void finalize(hipStream_t st) {
+    CFDJ_FFT(rocfft_execution_info_create(&info));
+    CFDJ_FFT(rocfft_execution_info_set_stream(info, st));
+    if (work_bytes) {
+      CFDJ_HIP(hipMalloc(&work, work_bytes));
+      CFDJ_FFT(rocfft_execution_info_set_work_buffer(info, work, work_bytes));
+    }
+  }
+  void exec(rocfft_plan p, const void* in, void* out) {
+    void* ib[1] = {const_cast<void*>(in)};
+    void* ob[1] = {out};
+    CFDJ_FFT(rocfft_execute(p, ib, out ? ob : nullptr, info));
+  }
+  void destroy() {
+    for (auto p : plans) rocfft_plan_destroy(p);
+    plans.clear();
+    if (info) rocfft_execution_info_destroy(info);
+    info = nullptr;
+    if (work) (void)hipFree(work);
+    work = nullptr;
+  }
+};
+
+// exp(-2 pi i k / n), k < n, rounded from long double (x86 80-bit) arithmetic.
+inline double2* twiddle_table(int n) {
+  const long double pi = 3.141592653589793238462643383279502884L;
+  std::vector<double2> h(n);
+  for (int k = 0; k < n; ++k) {
+    const long double a = 2.0L * pi * (long double)k / (long double)n;
+    h[k] = make_double2((double)cosl(a), (double)-sinl(a));
+  }
+  double2* d = dalloc<double2>(n);
+  CFDJ_HIP(hipMemcpy(d, h.data(), n * sizeof(double2), hipMemcpyHostToDevice));
+  return d;
+}
+
+// Hand-written 3-pass FFT Poisson (poisson_fft.hip) state: twiddle tables.
+struct Fused {
+  int n = 0, ncu = 256;
+  double2* twL = nullptr;
+  double2* twN = nullptr;
+  void init(int n_) {
+    n = n_;
+    int dev = 0;
+    CFDJ_HIP(hipGetDevice(&dev));
+    CFDJ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+    twL = twiddle_table(n / 2);
+    twN = twiddle_table(n);
+  }
+  void destroy() {
+    dfree(twL);
+    dfree(twN);
+  }
+  FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H,
+                        bool neg) const {
+    FusedPoissonArgs a;
+    a.n = n;
+    a.f = f;
+    a.s = s;
+    a.H = H;
+    a.twL = twL;
+    a.twN = twN;
+    a.cx = sym.cx;
+    a.cy = sym.cy;
+    a.aa = sym.aa;
+    a.bb = sym.bb;
+    a.cc = sym.cc;
+    a.scale = sym.scale;
+    a.neg = neg;
+    a.ncu = ncu;
+    return a;
+  }
+};
+
+// Poisson path selection (cfdj_vm_set_poisson / cfdj_fps_set_poisson).
+inline bool resolve_fused(int path, int nx, int ny, bool slab) {
+  if (path == CFDJ_POISSON_ROCFFT) return false;
+  const bool ok = !slab && fused_poisson_supported(nx, ny);
+  if (path == CFDJ_POISSON_FUSED && !ok)
+    throw Error{CFDJ_ERR_ARG, "fused Poisson needs a single-GPU square grid of 1024, 2048 "
+                              "or 4096 points per side"};
+  return ok;
+}
+
+}  // namespace cfdj

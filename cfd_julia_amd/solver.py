@@ -15,13 +15,20 @@ class PoissonFFT:
     """Periodic FD-FFT Poisson solver, plan built once (Common.jl:97-125 `fps`,
     12_Poisson_Solver_FFT/fft_p.jl:8-42 `ps_fft`)."""
 
-    def __init__(self, nx, ny, dx, dy, eps=1e-6, device=-1):
+    def __init__(self, nx, ny, dx, dy, eps=1e-6, device=-1, symbol="fd"):
+        """symbol: "fd" (Common.jl fps / fft_p.jl) or "spectral" (fft_s.jl ps_spectral)."""
         lib = _lib.load()
         _lib.require_gpu()
         h = C.c_void_p()
         check(lib.cfdj_fps_create(int(nx), int(ny), float(dx), float(dy), float(eps),
                                   int(device), C.byref(h)), "cfdj_fps_create")
         self._h, self.nx, self.ny = h, int(nx), int(ny)
+        if symbol != "fd":
+            kinds = {"spectral": _lib.SYMBOL_SPECTRAL}
+            if symbol not in kinds:
+                self.close()
+                raise ValueError(f"unknown symbol {symbol!r}")
+            check(lib.cfdj_fps_set_symbol(h, kinds[symbol]), "cfdj_fps_set_symbol")
 
     def solve(self, f, out=None):
         """f: (>=nx, >=ny) float64 array -> s: nx-by-ny (Fortran order)."""

@@ -48,6 +48,10 @@ extern "C" {
 #define CFDJ_POISSON_ROCFFT 1 /* rocFFT D2Z + divide kernel + rocFFT Z2D */
 #define CFDJ_POISSON_FUSED 2  /* hand-written 3-pass FFT (square 1024/2048/4096 grids) */
 
+/* Poisson symbol (cfdj_fps_set_symbol). */
+#define CFDJ_SYMBOL_FD 0       /* Common.jl:119-121 / fft_p.jl:37-39: aa + bb cos kx + cc cos ky */
+#define CFDJ_SYMBOL_SPECTRAL 1 /* 13_Poisson_Solver_FFT_Spectral/fft_s.jl:32-34: -kx^2 - ky^2 */
+
 typedef struct cfdj_vm cfdj_vm;   /* periodic vortex-merger solver state */
 typedef struct cfdj_fps_plan cfdj_fps_plan; /* periodic FD-FFT Poisson solver */
 
@@ -72,6 +76,9 @@ int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long 
 int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
 /* Select the Poisson implementation (CFDJ_POISSON_*); ARG error if unsupported. */
 int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path);
+/* Select the symbol: CFDJ_SYMBOL_FD (default, fps/ps_fft) or CFDJ_SYMBOL_SPECTRAL
+ * (fft_s.jl:8-37 ps_spectral: kx = 2pi/(nx dx) * index, kx[1] = eps, ky = kx). */
+int cfdj_fps_set_symbol(cfdj_fps_plan* h, int kind);
 void cfdj_fps_destroy(cfdj_fps_plan* h);
 /* One-shot convenience with the reference's per-call semantics. */
 int cfdj_fps(int nx, int ny, double dx, double dy, double eps, const double* f, long ldf,

@@ -336,3 +336,25 @@ def test_gpu_graph_timing_many_steps(cfdj):
         w_eager = h.download_interior()
     assert t["stage"][1] == 150 and t["fft_fwd"][1] == 150 and t["fft_inv"][1] == 150
     assert np.array_equal(w_graph, w_eager)
+
+
+# ---- spectral Poisson (13_Poisson_Solver_FFT_Spectral/fft_s.jl) --------------------------
+@pytest.mark.parametrize("i", range(5))
+def test_gpu_fft_s_matches_order_jl(cfdj, i):
+    from cfd_julia_amd import fft_s
+
+    n = vo.ORDER_JL_GRID[i]
+    l2, _ = fft_s.main(grids=(n,))[n]
+    ref = vo.ORDER_JL_FFT_SPECTRAL[i]  # round-off: only the magnitude is comparable
+    assert 0.3 * ref < l2 < 3.0 * ref, (n, l2, ref)
+
+
+@pytest.mark.parametrize("n,path", [(64, "rocfft"), (1024, "fused"), (1024, "rocfft")])
+def test_gpu_spectral_vs_oracle(cfdj, n, path):
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    f = smooth_field(n, n, 4, 51)
+    ref = vo.ps_spectral(f, dx, dy)
+    with cfdj.PoissonFFT(n, n, dx, dy, symbol="spectral") as h:
+        h.set_poisson(path)
+        s = h.solve(np.asfortranarray(f))
+    assert np.abs(s - ref).max() <= 1e-12 * np.abs(ref).max()
