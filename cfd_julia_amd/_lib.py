@@ -23,6 +23,7 @@ K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
 POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED = 0, 1, 2
 SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1
+CAVITY_DST, CAVITY_MG = 0, 1
 
 
 class CfdjError(RuntimeError):
@@ -79,6 +80,23 @@ SIGNATURES = {
     "cfdj_fps_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_fps_set_symbol": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_destroy": (None, [_vp]),
+    "cfdj_cavity_create": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                     C.c_int, C.POINTER(_vp)]),
+    "cfdj_cavity_set_poisson": (C.c_int, [_vp, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                          C.c_double, C.c_int]),
+    "cfdj_cavity_upload": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long]),
+    "cfdj_cavity_download": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long]),
+    "cfdj_cavity_step": (C.c_int, [_vp, C.c_double, C.c_int, _dp]),
+    "cfdj_cavity_rhs": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long, _dp, C.c_long]),
+    "cfdj_cavity_mg_iterations": (C.c_long, [_vp]),
+    "cfdj_cavity_destroy": (None, [_vp]),
+    "cfdj_fps_sine": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, _dp, C.c_long, _dp,
+                                C.c_long]),
+    "cfdj_mg_create": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, C.c_int, C.c_int,
+                                 C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "cfdj_mg_solve": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long, C.c_double, C.c_int, _ip,
+                                _dp]),
+    "cfdj_mg_destroy": (None, [_vp]),
 }
 
 _lock = threading.Lock()

@@ -1,0 +1,733 @@
+// Lid-driven cavity (18_NS2D_Lid_Driven_Cavity/lid_driven_cavity.jl) and n-level V-cycle
+// multigrid (17_Poisson_Solver_Multigrid/mg_N.jl + Common.jl:21-92,229-246) on gfx950.
+//
+// Fields are (nx+1) x (ny+1) node arrays, x contiguous, pitch nx+2 (even: 16-B rows).
+// Stencil / boundary / multigrid kernels keep the reference's expression order and are
+// compiled without FMA contraction (Makefile), so given the same inputs they reproduce the
+// CPU oracle bit for bit.  The DST-I Poisson (fps_sine) runs as the periodic FFT Poisson
+// of the odd-odd extension onto a (2nx) x (2ny) grid with the reference's iden multiplier
+// (host_common.hpp, kSymbolDirichletExt), so the C4 cavity at 2048^2 uses the fused 3-pass
+// FFT kernels on a 4096^2 extension.
+#include "host_common.hpp"
+
+namespace cfdj {
+
+namespace {
+
+constexpr int kBX = 64, kBY = 4;
+
+struct CavCoef {
+  double aa, bb, gg, hh, dt, c25dt, c13, c23, c23dt;
+};
+
+// lid_driven_cavity.jl:124-159 at interior node (i, j); gg inside each term.
+__device__ __forceinline__ double cavity_rhs_at(const double* __restrict__ w,
+                                                const double* __restrict__ s, size_t c,
+                                                int P, const CavCoef& k) {
+  const double wc = w[c];
+  const double wE = w[c + 1], wW = w[c - 1], wN = w[c + P], wS = w[c - P];
+  const double wNE = w[c + P + 1], wSW = w[c - P - 1], wNW = w[c + P - 1], wSE = w[c - P + 1];
+  const double sE = s[c + 1], sW = s[c - 1], sN = s[c + P], sS = s[c - P];
+  const double sNE = s[c + P + 1], sSW = s[c - P - 1], sNW = s[c + P - 1], sSE = s[c - P + 1];
+  const double j1 = k.gg * ((wE - wW) * (sN - sS) - (wN - wS) * (sE - sW));
+  const double j2 =
+      k.gg * (wE * (sNE - sSE) - wW * (sNW - sSW) - wN * (sNE - sNW) + wS * (sSE - sSW));
+  const double j3 =
+      k.gg * (wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS));
+  const double jac = (j1 + j2 + j3) * k.hh;
+  return -jac + (k.aa * (wE - 2.0 * wc + wW) + k.bb * (wN - 2.0 * wc + wS));
+}
+
+// Stage updates of lid_driven_cavity.jl:80, 89-93, 102-106 (interior only).
+template <int STAGE>
+__global__ __launch_bounds__(kBX* kBY) void cavity_stage_kernel(
+    const double* __restrict__ w, const double* __restrict__ s, const double* wn, double* out,
+    int nx, int ny, int P, CavCoef k) {
+  const int i = 1 + blockIdx.x * kBX + threadIdx.x;
+  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
+  if (i >= nx || j >= ny) return;
+  const size_t c = (size_t)j * P + i;
+  const double r = cavity_rhs_at(w, s, c, P, k);
+  double o;
+  if constexpr (STAGE == 0) {
+    o = r;
+  } else if constexpr (STAGE == 1) {
+    o = w[c] + k.dt * r;
+  } else if constexpr (STAGE == 2) {
+    o = (0.75 * wn[c] + 0.25 * w[c]) + k.c25dt * r;
+  } else {
+    o = (k.c13 * wn[c] + k.c23 * w[c]) + k.c23dt * r;
+  }
+  out[c] = o;
+}
+
+// lid_driven_cavity.jl:39-51: Jensen wall vorticity.  The reference's bottom/top loop runs
+// second and overwrites the corners, so corners take the bottom/top formula.
+__global__ __launch_bounds__(256) void bc2_kernel(double* __restrict__ w,
+                                                  const double* __restrict__ s, int nx,
+                                                  int ny, int P, double dx2, double dy2,
+                                                  double dy) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t <= nx) {  // bottom (j = 0) and top (j = ny) rows, all i
+    const int i = t;
+    w[i] = (-4.0 * s[(size_t)P + i] + 0.5 * s[(size_t)2 * P + i]) / dy2;
+    w[(size_t)ny * P + i] =
+        (-4.0 * s[(size_t)(ny - 1) * P + i] + 0.5 * s[(size_t)(ny - 2) * P + i]) / dy2 -
+        3.0 / dy;
+  } else if (t <= nx + ny - 1) {  // left / right columns, j = 1..ny-1
+    const int j = t - nx;
+    const size_t r = (size_t)j * P;
+    w[r] = (-4.0 * s[r + 1] + 0.5 * s[r + 2]) / dx2;
+    w[r + nx] = (-4.0 * s[r + nx - 1] + 0.5 * s[r + nx - 2]) / dx2;
+  }
+}
+
+// Odd-odd extension of the interior of w onto the (2nx) x (2ny) periodic grid (pitch 2nx):
+// E(i', j') = sx sy w(|i|, |j|), zero on the lines i' in {0, nx}, j' in {0, ny}.
+__global__ __launch_bounds__(256) void odd_extend_kernel(const double* __restrict__ w,
+                                                         double* __restrict__ E, int nx,
+                                                         int ny, int P) {
+  const int ip = blockIdx.x * blockDim.x + threadIdx.x;
+  const int jp = blockIdx.y;
+  if (ip >= 2 * nx) return;
+  const int i = ip <= nx ? ip : 2 * nx - ip;
+  const int j = jp <= ny ? jp : 2 * ny - jp;
+  double v = 0.0;
+  if (i != 0 && i != nx && j != 0 && j != ny) {
+    v = w[(size_t)j * P + i];
+    if ((ip > nx) != (jp > ny)) v = -v;
+  }
+  E[(size_t)jp * (2 * nx) + ip] = v;
+}
+
+// s[i, j] = psi_ext[j][i] on the interior (the reference's sn boundary stays untouched).
+__global__ __launch_bounds__(256) void extract_kernel(const double* __restrict__ X,
+                                                      double* __restrict__ s, int nx, int ny,
+                                                      int P) {
+  const int i = 1 + blockIdx.x * blockDim.x + threadIdx.x;
+  const int j = 1 + blockIdx.y;
+  if (i >= nx) return;
+  s[(size_t)j * P + i] = X[(size_t)j * (2 * nx) + i];
+}
+
+// Deterministic two-pass sum of squares over an n0 x n1 block (pitch P) of (a - b) or a.
+__global__ __launch_bounds__(256) void sumsq_partial_kernel(const double* __restrict__ a,
+                                                            const double* __restrict__ b,
+                                                            int i0, int n0, int j0, int n1,
+                                                            int P, double* __restrict__ part) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  const long total = (long)n0 * n1;
+  for (long e = blockIdx.x * (long)blockDim.x + threadIdx.x; e < total;
+       e += (long)gridDim.x * blockDim.x) {
+    const int j = (int)(e / n0), i = (int)(e % n0);
+    const size_t c = (size_t)(j0 + j) * P + (i0 + i);
+    const double d = b ? a[c] - b[c] : a[c];
+    acc += d * d;
+  }
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void sumsq_final_kernel(const double* __restrict__ part,
+                                                          int nparts, double denom,
+                                                          double* __restrict__ out) {
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = sqrt(red[0] / denom);
+}
+
+// ---- multigrid (Common.jl) ------------------------------------------------------------
+// One red-black half sweep of the Common.jl:84-88 update on points with (i + j) % 2 ==
+// parity (the reference's lexicographic order is inherently serial; converged solutions
+// agree to the solver tolerance, tests/test_gpu_cavity.py).
+__global__ __launch_bounds__(kBX* kBY) void rbgs_kernel(const double* __restrict__ f,
+                                                        double* __restrict__ u, int nx, int ny,
+                                                        int P, double dx2, double dy2,
+                                                        double dd, int parity) {
+  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
+  const int i = 1 + 2 * (blockIdx.x * kBX + threadIdx.x) + ((j + 1 + parity) & 1);
+  if (i >= nx || j >= ny) return;
+  const size_t c = (size_t)j * P + i;
+  const double uc = u[c];
+  const double rt = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 +
+                            (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
+  u[c] = uc + rt / dd;
+}
+
+// Common.jl:239-246
+__global__ __launch_bounds__(kBX* kBY) void residual_kernel(const double* __restrict__ f,
+                                                            const double* __restrict__ u,
+                                                            double* __restrict__ r, int nx,
+                                                            int ny, int P, double dx2,
+                                                            double dy2) {
+  const int i = 1 + blockIdx.x * kBX + threadIdx.x;
+  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
+  if (i >= nx || j >= ny) return;
+  const size_t c = (size_t)j * P + i;
+  const double uc = u[c];
+  r[c] = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 + (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
+}
+
+// Common.jl:21-48: full weighting on the coarse interior, injection on its boundary.
+__global__ __launch_bounds__(kBX* kBY) void restriction_kernel(const double* __restrict__ r,
+                                                               double* __restrict__ ec, int nxf,
+                                                               int nyf, int Pf, int nxc,
+                                                               int nyc, int Pc) {
+  const int i = blockIdx.x * kBX + threadIdx.x;  // 0..nxc
+  const int j = blockIdx.y * kBY + threadIdx.y;  // 0..nyc
+  if (i > nxc || j > nyc) return;
+  double v;
+  if (i == 0 || i == nxc || j == 0 || j == nyc) {
+    // the reference's boundary loops: bottom/top (i = 1, nxc+1: rows of r) run first, then
+    // left/right (j = 1, nyc+1) overwrite the corners -- both inject the same node
+    v = r[(size_t)(j == 0 ? 0 : (j == nyc ? nyf : 2 * j)) * Pf +
+          (i == 0 ? 0 : (i == nxc ? nxf : 2 * i))];
+  } else {
+    const size_t c = (size_t)(2 * j) * Pf + 2 * i;
+    const double center = 4.0 * r[c];
+    const double grid = 2.0 * (r[c + Pf] + r[c - Pf] + r[c + 1] + r[c - 1]);
+    const double corner = r[c + Pf + 1] + r[c - Pf + 1] + r[c + Pf - 1] + r[c - Pf - 1];
+    v = (center + grid + corner) / 16.0;
+  }
+  ec[(size_t)j * Pc + i] = v;
+}
+
+// Common.jl:50-76 + mg_N.jl:99-101: u_f[interior] += bilinear prolongation of u_c.
+__global__ __launch_bounds__(kBX* kBY) void prolong_add_kernel(const double* __restrict__ uc,
+                                                               double* __restrict__ uf, int nxf,
+                                                               int nyf, int Pf, int Pc) {
+  const int I = 1 + blockIdx.x * kBX + threadIdx.x;
+  const int J = 1 + blockIdx.y * kBY + threadIdx.y;
+  if (I >= nxf || J >= nyf) return;
+  const int ic = I >> 1, jc = J >> 1;
+  const size_t c = (size_t)jc * Pc + ic;
+  double p;
+  if (!(I & 1) && !(J & 1)) {
+    p = uc[c];
+  } else if (!(I & 1)) {  // J odd: ef[2i-1, 2j] = .5(unc[i,j] + unc[i,j+1])
+    p = 0.5 * (uc[c] + uc[c + Pc]);
+  } else if (!(J & 1)) {  // I odd: ef[2i, 2j-1] = .5(unc[i,j] + unc[i+1,j])
+    p = 0.5 * (uc[c] + uc[c + 1]);
+  } else {
+    p = 0.25 * (uc[c] + uc[c + Pc] + uc[c + 1] + uc[c + Pc + 1]);
+  }
+  uf[(size_t)J * Pf + I] += p;
+}
+
+__global__ __launch_bounds__(256) void negate_kernel(const double* __restrict__ a,
+                                                     double* __restrict__ b, size_t n) {
+  const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (e < n) b[e] = -a[e];
+}
+
+dim3 interior_grid(int nx, int ny) {
+  return dim3((nx - 1 + kBX - 1) / kBX, (ny - 1 + kBY - 1) / kBY);
+}
+
+}  // namespace
+
+// ---- host objects ----------------------------------------------------------------------
+// Device-side reduction: rms written to *out (device pointer).
+static void launch_rms(const double* a, const double* b, int i0, int n0, int j0, int n1, int P,
+                       double denom, double* part, int nparts, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_partial_kernel, dim3(nparts), dim3(256), 0, st, a, b, i0, n0, j0,
+                     n1, P, part);
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, st, part, nparts, denom, out);
+  CFDJ_HIP(hipGetLastError());
+}
+
+// n-level V-cycle (mg_N.jl:7-114) on device buffers.
+struct Multigrid {
+  int nlev = 0, v1 = 2, v2 = 2, v3 = 2;
+  std::vector<int> lnx, lny, lP;
+  std::vector<double> ldx, ldy;
+  std::vector<double*> u, f, r;  // level 0 u/f may alias caller buffers
+  double* part = nullptr;
+  double* d_rms = nullptr;
+  static constexpr int kParts = 512;
+  hipStream_t st = nullptr;
+
+  void init(int nx, int ny, double dx, double dy, int n_level, int v1_, int v2_, int v3_,
+            hipStream_t s) {
+    CFDJ_REQUIRE(n_level >= 1, "n_level must be >= 1");
+    CFDJ_REQUIRE((nx >> (n_level - 1)) >= 2 && (ny >> (n_level - 1)) >= 2,
+                 "n_level exceeds the possible number of levels (mg_N.jl:26)");
+    CFDJ_REQUIRE(nx % (1 << (n_level - 1)) == 0 && ny % (1 << (n_level - 1)) == 0,
+                 "nx, ny must be divisible by 2^(n_level-1)");
+    nlev = n_level;
+    v1 = v1_;
+    v2 = v2_;
+    v3 = v3_;
+    st = s;
+    for (int l = 0; l < nlev; ++l) {
+      lnx.push_back(l ? lnx[l - 1] / 2 : nx);
+      lny.push_back(l ? lny[l - 1] / 2 : ny);
+      lP.push_back(lnx[l] + 2);
+      ldx.push_back(l ? 2.0 * ldx[l - 1] : dx);
+      ldy.push_back(l ? 2.0 * ldy[l - 1] : dy);
+      const size_t n = (size_t)lP[l] * (lny[l] + 1);
+      u.push_back(l ? dalloc<double>(n) : nullptr);
+      f.push_back(l ? dalloc<double>(n) : nullptr);
+      r.push_back(dalloc<double>(n));
+      CFDJ_HIP(hipMemset(r[l], 0, n * sizeof(double)));
+      if (l) CFDJ_HIP(hipMemset(f[l], 0, n * sizeof(double)));
+    }
+    part = dalloc<double>(kParts);
+    d_rms = dalloc<double>(1);
+  }
+  void destroy() {
+    for (int l = 1; l < nlev; ++l) {
+      dfree(u[l]);
+      dfree(f[l]);
+    }
+    for (auto& p : r) dfree(p);
+    dfree(part);
+    dfree(d_rms);
+  }
+  void smooth(int l, int sweeps) {
+    const double dx2 = ldx[l] * ldx[l], dy2 = ldy[l] * ldy[l];
+    const double dd = -2.0 / dx2 - 2.0 / dy2;
+    dim3 g((lnx[l] / 2 + kBX - 1) / kBX, (lny[l] - 1 + kBY - 1) / kBY);
+    for (int s = 0; s < sweeps; ++s)
+      for (int parity = 0; parity < 2; ++parity)
+        hipLaunchKernelGGL(rbgs_kernel, g, dim3(kBX, kBY), 0, st, f[l], u[l], lnx[l], lny[l],
+                           lP[l], dx2, dy2, dd, parity);
+    CFDJ_HIP(hipGetLastError());
+  }
+  void residual(int l) {
+    hipLaunchKernelGGL(residual_kernel, interior_grid(lnx[l], lny[l]), dim3(kBX, kBY), 0, st,
+                       f[l], u[l], r[l], lnx[l], lny[l], lP[l], ldx[l] * ldx[l],
+                       ldy[l] * ldy[l]);
+    CFDJ_HIP(hipGetLastError());
+  }
+  double l2norm0() {  // Common.jl:229-232 on level 0's residual (host sync)
+    launch_rms(r[0], nullptr, 1, lnx[0] - 1, 1, lny[0] - 1, lP[0],
+               (double)(lnx[0] - 1) * (lny[0] - 1), part, kParts, d_rms, st);
+    double h = 0.0;
+    CFDJ_HIP(hipMemcpyAsync(&h, d_rms, sizeof(double), hipMemcpyDeviceToHost, st));
+    CFDJ_HIP(hipStreamSynchronize(st));
+    return h;
+  }
+  // Solve on level-0 buffers u0 (in/out, boundary = Dirichlet data) and f0 (pitch nx+2).
+  int solve(double* u0, double* f0, double tol, int max_iter, std::vector<double>* hist) {
+    u[0] = u0;
+    f[0] = f0;
+    residual(0);
+    const double init_rms = l2norm0();
+    double rms = init_rms;
+    if (hist) hist->push_back(rms);
+    int it = 0;
+    while (it < max_iter) {
+      ++it;
+      smooth(0, v1);
+      residual(0);
+      rms = l2norm0();
+      if (hist) hist->push_back(rms);
+      if (!(rms / init_rms > tol)) break;  // also stops on init_rms == 0
+      for (int k = 1; k < nlev; ++k) {
+        if (k > 1) residual(k - 1);
+        hipLaunchKernelGGL(restriction_kernel,
+                           dim3((lnx[k] + 1 + kBX - 1) / kBX, (lny[k] + 1 + kBY - 1) / kBY),
+                           dim3(kBX, kBY), 0, st, r[k - 1], f[k], lnx[k - 1], lny[k - 1],
+                           lP[k - 1], lnx[k], lny[k], lP[k]);
+        CFDJ_HIP(hipMemsetAsync(u[k], 0, (size_t)lP[k] * (lny[k] + 1) * sizeof(double), st));
+        smooth(k, k < nlev - 1 ? v1 : v2);
+      }
+      for (int k = nlev - 1; k >= 1; --k) {
+        hipLaunchKernelGGL(prolong_add_kernel, interior_grid(lnx[k - 1], lny[k - 1]),
+                           dim3(kBX, kBY), 0, st, u[k], u[k - 1], lnx[k - 1], lny[k - 1],
+                           lP[k - 1], lP[k]);
+        smooth(k - 1, v3);
+      }
+      CFDJ_HIP(hipGetLastError());
+    }
+    return it;
+  }
+};
+
+}  // namespace cfdj
+
+using namespace cfdj;
+
+// =====================================================================================
+// Multigrid handle (mg_N.jl:7-114)
+// =====================================================================================
+struct cfdj_mg {
+  int device = -1, nx = 0, ny = 0;
+  hipStream_t stream = nullptr;
+  Multigrid mg;
+  double *u = nullptr, *f = nullptr;
+  ~cfdj_mg() {
+    mg.destroy();
+    dfree(u);
+    dfree(f);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+// =====================================================================================
+// Lid-driven cavity handle (lid_driven_cavity.jl:58-118)
+// =====================================================================================
+struct cfdj_cavity {
+  int device = -1, nx = 0, ny = 0, P = 0;
+  double dx = 0, dy = 0, re = 0;
+  hipStream_t stream = nullptr;
+  double *wn = nullptr, *wa = nullptr, *wb = nullptr;  // omega^n and the two stage buffers
+  double *sn = nullptr, *sp = nullptr;                 // psi and the previous step's psi
+  // DST Poisson on the odd-odd (2nx) x (2ny) extension
+  Symbol sym;
+  Plans plans;
+  rocfft_plan fwd = nullptr, inv = nullptr;
+  Fused fused;
+  bool use_fused = false;
+  double* ext = nullptr;   // extension / psi_ext (2nx x 2ny real)
+  double* ext2 = nullptr;  // rocFFT path output
+  double2* spec = nullptr;
+  // multigrid alternative
+  int poisson = CFDJ_CAVITY_DST;
+  Multigrid mg;
+  bool mg_ready = false;
+  double mg_tol = 1e-9;
+  int mg_max_iter = 100000;
+  double* mg_f = nullptr;
+  long mg_iters = 0;
+  // rms
+  double* part = nullptr;
+  double* d_rms = nullptr;
+  int rms_cap = 0;
+  static constexpr int kParts = 512;
+
+  size_t field() const { return (size_t)P * (ny + 1); }
+
+  void dst_poisson(const double* w, double* s) {  // s_interior = fps_sine(-w)
+    const int NX = 2 * nx, NY = 2 * ny;
+    hipLaunchKernelGGL(odd_extend_kernel, dim3((NX + 255) / 256, NY), dim3(256), 0, stream, w,
+                       ext, nx, ny, P);
+    CFDJ_HIP(hipGetLastError());
+    double* psi = ext;
+    if (use_fused) {
+      const FusedPoissonArgs a = fused.args(sym, ext, ext, spec, true);
+      for (int pass = 0; pass < 3; ++pass) launch_fused_poisson_pass(pass, a, stream);
+    } else {
+      plans.exec(fwd, ext, spec);
+      launch_divide(sym.divide(spec, sym.nxh, NY, sym.nxh, 0, true), stream);
+      plans.exec(inv, spec, ext2);
+      psi = ext2;
+    }
+    hipLaunchKernelGGL(extract_kernel, dim3((nx - 1 + 255) / 256, ny - 1), dim3(256), 0, stream,
+                       psi, s, nx, ny, P);
+    CFDJ_HIP(hipGetLastError());
+  }
+
+  void mg_poisson(const double* w, double* s) {  // s (warm start, boundary 0) <- MG(-w)
+    hipLaunchKernelGGL(negate_kernel, dim3((unsigned)((field() + 255) / 256)), dim3(256), 0,
+                       stream, w, mg_f, field());
+    CFDJ_HIP(hipGetLastError());
+    mg_iters += mg.solve(s, mg_f, mg_tol, mg_max_iter, nullptr);
+  }
+
+  void poisson_solve(const double* w, double* s) {
+    if (poisson == CFDJ_CAVITY_MG) mg_poisson(w, s);
+    else dst_poisson(w, s);
+  }
+
+  CavCoef coef(double dt) const {
+    CavCoef k;
+    k.aa = 1.0 / (re * (dx * dx));
+    k.bb = 1.0 / (re * (dy * dy));
+    k.gg = 1.0 / ((4.0 * dx) * dy);
+    k.hh = 1.0 / 3.0;
+    k.dt = dt;
+    k.c25dt = 0.25 * dt;
+    k.c13 = 1.0 / 3.0;
+    k.c23 = 2.0 / 3.0;
+    k.c23dt = (2.0 / 3.0) * dt;
+    return k;
+  }
+
+  void stage(int st_, const double* w, double* out, double dt) {
+    const CavCoef k = coef(dt);
+    const dim3 g = interior_grid(nx, ny), b(kBX, kBY);
+    switch (st_) {
+      case 0: hipLaunchKernelGGL(cavity_stage_kernel<0>, g, b, 0, stream, w, sn, wn, out, nx, ny, P, k); break;
+      case 1: hipLaunchKernelGGL(cavity_stage_kernel<1>, g, b, 0, stream, w, sn, wn, out, nx, ny, P, k); break;
+      case 2: hipLaunchKernelGGL(cavity_stage_kernel<2>, g, b, 0, stream, w, sn, wn, out, nx, ny, P, k); break;
+      default: hipLaunchKernelGGL(cavity_stage_kernel<3>, g, b, 0, stream, w, sn, wn, out, nx, ny, P, k); break;
+    }
+    CFDJ_HIP(hipGetLastError());
+  }
+
+  void bc2(double* w) {
+    hipLaunchKernelGGL(bc2_kernel, dim3((nx + ny + 255) / 256), dim3(256), 0, stream, w, sn,
+                       nx, ny, P, dx * dx, dy * dy, dy);
+    CFDJ_HIP(hipGetLastError());
+  }
+
+  // lid_driven_cavity.jl:75-114; rms of step k into d_rms[k]
+  void step(double dt, int k) {
+    CFDJ_HIP(hipMemcpyAsync(sp, sn, field() * sizeof(double), hipMemcpyDeviceToDevice, stream));
+    stage(1, wn, wa, dt);  // wt = wn + dt r(wn, sn)
+    bc2(wa);
+    poisson_solve(wa, sn);
+    stage(2, wa, wb, dt);  // wt = (.75wn + .25wt) + .25dt r(wt, sn)
+    bc2(wb);
+    poisson_solve(wb, sn);
+    stage(3, wb, wn, dt);  // wn = ((1/3)wn + (2/3)wt) + (2/3)dt r(wt, sn)
+    bc2(wn);
+    poisson_solve(wn, sn);
+    launch_rms(sn, sp, 0, nx + 1, 0, ny + 1, P, (double)(nx + 1) * (ny + 1), part, kParts,
+               d_rms + k, stream);
+  }
+
+  ~cfdj_cavity() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    dfree(wn);
+    dfree(wa);
+    dfree(wb);
+    dfree(sn);
+    dfree(sp);
+    sym.destroy();
+    plans.destroy();
+    fused.destroy();
+    dfree(ext);
+    dfree(ext2);
+    dfree(spec);
+    if (mg_ready) mg.destroy();
+    dfree(mg_f);
+    dfree(part);
+    dfree(d_rms);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+namespace {
+
+void copy_in(double* d, int P, const double* h, long ld, int nx, int ny, hipStream_t st) {
+  CFDJ_HIP(hipMemcpy2DAsync(d, P * sizeof(double), h, ld * sizeof(double),
+                            (nx + 1) * sizeof(double), ny + 1, hipMemcpyHostToDevice, st));
+}
+void copy_out(double* h, long ld, const double* d, int P, int nx, int ny, hipStream_t st) {
+  CFDJ_HIP(hipMemcpy2DAsync(h, ld * sizeof(double), d, P * sizeof(double),
+                            (nx + 1) * sizeof(double), ny + 1, hipMemcpyDeviceToHost, st));
+}
+
+}  // namespace
+
+extern "C" {
+
+int cfdj_cavity_create(int nx, int ny, double dx, double dy, double re, int device,
+                       cfdj_cavity** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr, "out is NULL");
+    *out = nullptr;
+    CFDJ_REQUIRE(nx >= 4 && ny >= 4, "nx, ny must be >= 4 (bc2 reads s[3, j])");
+    CFDJ_REQUIRE(dx > 0 && dy > 0 && std::isfinite(re) && re != 0.0, "bad dx, dy or re");
+    fft_setup();
+    select_device(device);
+    std::unique_ptr<cfdj_cavity> h(new cfdj_cavity);
+    CFDJ_HIP(hipGetDevice(&h->device));
+    CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->nx = nx;
+    h->ny = ny;
+    h->dx = dx;
+    h->dy = dy;
+    h->re = re;
+    h->P = nx + 2;
+    const size_t n = h->field();
+    for (double** p : {&h->wn, &h->wa, &h->wb, &h->sn, &h->sp}) {
+      *p = dalloc<double>(n);
+      CFDJ_HIP(hipMemset(*p, 0, n * sizeof(double)));
+    }
+    const int NX = 2 * nx, NY = 2 * ny;
+    h->sym.init(NX, NY, dx, dy, 0.0, kSymbolDirichletExt);
+    h->ext = dalloc<double>((size_t)NX * NY);
+    h->spec = dalloc<double2>((size_t)(NX / 2 + 1) * NY);
+    if (fused_poisson_supported(NX, NY)) {
+      h->fused.init(NX);
+      h->use_fused = true;
+    } else {
+      size_t lens[2] = {(size_t)NX, (size_t)NY};
+      h->fwd = h->plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace, 2,
+                            lens, 1, nullptr);
+      h->inv = h->plans.add(rocfft_transform_type_real_inverse, rocfft_placement_notinplace, 2,
+                            lens, 1, nullptr);
+      h->plans.finalize(h->stream);
+      h->ext2 = dalloc<double>((size_t)NX * NY);
+    }
+    h->part = dalloc<double>(cfdj_cavity::kParts);
+    *out = h.release();
+  });
+}
+
+int cfdj_cavity_set_poisson(cfdj_cavity* h, int solver, int n_level, int v1, int v2, int v3,
+                            double tol, int max_iter) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(solver == CFDJ_CAVITY_DST || solver == CFDJ_CAVITY_MG, "bad solver");
+    select_device(h->device);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    if (solver == CFDJ_CAVITY_MG) {
+      CFDJ_REQUIRE(tol > 0 && max_iter >= 1 && v1 >= 0 && v2 >= 0 && v3 >= 0, "bad MG args");
+      if (h->mg_ready) h->mg.destroy();
+      h->mg = Multigrid();
+      h->mg.init(h->nx, h->ny, h->dx, h->dy, n_level, v1, v2, v3, h->stream);
+      h->mg_ready = true;
+      if (!h->mg_f) {
+        h->mg_f = dalloc<double>(h->field());
+        CFDJ_HIP(hipMemset(h->mg_f, 0, h->field() * sizeof(double)));
+      }
+      h->mg_tol = tol;
+      h->mg_max_iter = max_iter;
+    }
+    h->poisson = solver;
+  });
+}
+
+int cfdj_cavity_upload(cfdj_cavity* h, const double* wn, long ldw, const double* sn, long lds) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && wn && sn, "NULL argument");
+    CFDJ_REQUIRE(ldw >= h->nx + 1 && lds >= h->nx + 1, "leading dimension too small");
+    select_device(h->device);
+    copy_in(h->wn, h->P, wn, ldw, h->nx, h->ny, h->stream);
+    copy_in(h->sn, h->P, sn, lds, h->nx, h->ny, h->stream);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_cavity_download(cfdj_cavity* h, double* wn, long ldw, double* sn, long lds) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && wn && sn, "NULL argument");
+    CFDJ_REQUIRE(ldw >= h->nx + 1 && lds >= h->nx + 1, "leading dimension too small");
+    select_device(h->device);
+    copy_out(wn, ldw, h->wn, h->P, h->nx, h->ny, h->stream);
+    copy_out(sn, lds, h->sn, h->P, h->nx, h->ny, h->stream);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_cavity_step(cfdj_cavity* h, double dt, int nsteps, double* rms) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(nsteps >= 0 && std::isfinite(dt), "bad dt / nsteps");
+    select_device(h->device);
+    if (nsteps > h->rms_cap) {
+      dfree(h->d_rms);
+      h->d_rms = dalloc<double>(nsteps);
+      h->rms_cap = nsteps;
+    }
+    for (int k = 0; k < nsteps; ++k) h->step(dt, k);
+    if (rms && nsteps)
+      CFDJ_HIP(hipMemcpyAsync(rms, h->d_rms, nsteps * sizeof(double), hipMemcpyDeviceToHost,
+                              h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_cavity_rhs(cfdj_cavity* h, const double* w, long ldw, const double* s, long lds,
+                    double* r, long ldr) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && w && s && r, "NULL argument");
+    CFDJ_REQUIRE(ldw >= h->nx + 1 && lds >= h->nx + 1 && ldr >= h->nx + 1, "bad ld");
+    select_device(h->device);
+    copy_in(h->wa, h->P, w, ldw, h->nx, h->ny, h->stream);
+    copy_in(h->sn, h->P, s, lds, h->nx, h->ny, h->stream);
+    CFDJ_HIP(hipMemsetAsync(h->wb, 0, h->field() * sizeof(double), h->stream));
+    h->stage(0, h->wa, h->wb, 0.0);
+    copy_out(r, ldr, h->wb, h->P, h->nx, h->ny, h->stream);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+long cfdj_cavity_mg_iterations(cfdj_cavity* h) { return h ? h->mg_iters : -1; }
+
+void cfdj_cavity_destroy(cfdj_cavity* h) {
+  if (!h) return;
+  (void)guard([&] {
+    select_device(h->device);
+    delete h;
+  });
+}
+
+int cfdj_fps_sine(int nx, int ny, double dx, double dy, const double* f, long ldf, double* s,
+                  long lds) {
+  cfdj_cavity* h = nullptr;
+  int rc = cfdj_cavity_create(nx, ny, dx, dy, 1.0, -1, &h);
+  if (rc != CFDJ_OK) return rc;
+  rc = guard([&] {
+    CFDJ_REQUIRE(f && s && ldf >= nx + 1 && lds >= nx + 1, "bad f / s");
+    copy_in(h->wa, h->P, f, ldf, nx, ny, h->stream);
+    copy_in(h->sn, h->P, s, lds, nx, ny, h->stream);
+    // fps_sine(f) solves with +f: dst_poisson negates, so feed -f
+    hipLaunchKernelGGL(negate_kernel, dim3((unsigned)((h->field() + 255) / 256)), dim3(256), 0,
+                       h->stream, h->wa, h->wb, h->field());
+    CFDJ_HIP(hipGetLastError());
+    h->dst_poisson(h->wb, h->sn);
+    copy_out(s, lds, h->sn, h->P, nx, ny, h->stream);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+  cfdj_cavity_destroy(h);
+  return rc;
+}
+
+// ---- multigrid -----------------------------------------------------------------------
+int cfdj_mg_create(int nx, int ny, double dx, double dy, int n_level, int v1, int v2, int v3,
+                   int device, cfdj_mg** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr, "out is NULL");
+    *out = nullptr;
+    CFDJ_REQUIRE(nx >= 2 && ny >= 2 && dx > 0 && dy > 0, "bad grid");
+    CFDJ_REQUIRE(v1 >= 0 && v2 >= 0 && v3 >= 0, "bad sweep counts");
+    select_device(device);
+    std::unique_ptr<cfdj_mg> h(new cfdj_mg);
+    CFDJ_HIP(hipGetDevice(&h->device));
+    CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->nx = nx;
+    h->ny = ny;
+    h->mg.init(nx, ny, dx, dy, n_level, v1, v2, v3, h->stream);
+    const size_t n = (size_t)(nx + 2) * (ny + 1);
+    h->u = dalloc<double>(n);
+    h->f = dalloc<double>(n);
+    *out = h.release();
+  });
+}
+
+int cfdj_mg_solve(cfdj_mg* h, const double* f, long ldf, double* u, long ldu, double tol,
+                  int max_iter, int* iterations, double* rms_hist) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && f && u, "NULL argument");
+    CFDJ_REQUIRE(ldf >= h->nx + 1 && ldu >= h->nx + 1, "leading dimension too small");
+    CFDJ_REQUIRE(tol >= 0 && max_iter >= 0, "bad tol / max_iter");
+    select_device(h->device);
+    copy_in(h->f, h->nx + 2, f, ldf, h->nx, h->ny, h->stream);
+    copy_in(h->u, h->nx + 2, u, ldu, h->nx, h->ny, h->stream);
+    std::vector<double> hist;
+    const int it = h->mg.solve(h->u, h->f, tol, max_iter, &hist);
+    copy_out(u, ldu, h->u, h->nx + 2, h->nx, h->ny, h->stream);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    if (iterations) *iterations = it;
+    if (rms_hist) std::memcpy(rms_hist, hist.data(), hist.size() * sizeof(double));
+  });
+}
+
+void cfdj_mg_destroy(cfdj_mg* h) {
+  if (!h) return;
+  (void)guard([&] {
+    select_device(h->device);
+    delete h;
+  });
+}
+
+}  // extern "C"

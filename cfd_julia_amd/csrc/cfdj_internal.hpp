@@ -105,6 +105,7 @@ struct DivideParams {
   int width, rows, pitch, kx_off, nxh;
   double aa, bb, cc, scale;
   bool neg;
+  bool recip;  // multiply by the rounded reciprocal (lid_driven_cavity.jl:17 e * iden)
 };
 void launch_divide(const DivideParams& p, hipStream_t st);
 
@@ -130,6 +131,7 @@ struct FusedPoissonArgs {
   const double* cy;     // cos(ky[k]), k < n
   double aa, bb, cc, scale;
   bool neg;
+  bool recip;           // see DivideParams::recip
   int ncu;              // compute units (persistent grid size)
 };
 bool fused_poisson_supported(int nx, int ny);

@@ -81,6 +81,9 @@ inline void check_grid(int nx, int ny, double dx, double dy) {
 }
 
 // ---- spectral symbol tables + constants (Common.jl:101-103, 119-121) ----------------
+// Internal symbol kind (not in the C header): the cavity's DST-I multiplier.
+constexpr int kSymbolDirichletExt = 100;
+
 struct Symbol {
   int nx = 0, ny = 0, nxh = 0, kind = CFDJ_SYMBOL_FD;
   double aa = 0, bb = 0, cc = 0, scale = 0;
@@ -106,6 +109,20 @@ struct Symbol {
       std::vector<double> kx = kx_table(nx, eps);
       for (int m = 0; m < nxh; ++m) hcx[m] = std::cos(kx[m]);
       for (int n = 0; n < ny; ++n) hcy[n] = std::cos(kx[n]);
+    } else if (kind == kSymbolDirichletExt) {
+      // Odd-odd extension of a (nx/2) x (ny/2)-cell Dirichlet box onto this nx x ny
+      // periodic grid: d = tx + ty with tx[m] = (2/dx^2)(cos(pi m/(nx/2)) - 1) (the
+      // reference's iden denominator, lid_driven_cavity.jl:64-69), applied as e * (1/d).
+      aa = 0.0;
+      bb = 1.0;
+      cc = 1.0;
+      const int cx_cells = nx / 2, cy_cells = ny / 2;
+      auto t = [](int k, int cells, double h) {
+        const int kk = k <= cells ? k : 2 * cells - k;  // exact even symmetry
+        return (2.0 / (h * h)) * (std::cos((M_PI * kk) / cells) - 1.0);
+      };
+      for (int m = 0; m < nxh; ++m) hcx[m] = t(m, cx_cells, dx);
+      for (int n = 0; n < ny; ++n) hcy[n] = t(n, cy_cells, dy);
     } else {
       aa = 0.0;
       bb = -1.0;
@@ -126,7 +143,7 @@ struct Symbol {
     cy = dalloc<double>(ny);
     CFDJ_HIP(hipMemcpy(cx, hcx.data(), nxh * sizeof(double), hipMemcpyHostToDevice));
     CFDJ_HIP(hipMemcpy(cy, hcy.data(), ny * sizeof(double), hipMemcpyHostToDevice));
-    if (ny != nx) {
+    if (ny != nx && kind != kSymbolDirichletExt) {  // the Dirichlet symbol is even
       std::vector<double> hm(ny);
       for (int n = 0; n < ny; ++n) hm[n] = hcy[(ny - n) % ny];
       cy_mirror = dalloc<double>(ny);
@@ -155,6 +172,7 @@ struct Symbol {
     p.cc = cc;
     p.scale = scale;
     p.neg = neg;
+    p.recip = kind == kSymbolDirichletExt;
     return p;
   }
 };
@@ -246,6 +264,7 @@ struct Fused {
     a.cc = sym.cc;
     a.scale = sym.scale;
     a.neg = neg;
+    a.recip = sym.kind == kSymbolDirichletExt;
     a.ncu = ncu;
     return a;
   }

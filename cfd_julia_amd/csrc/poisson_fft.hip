@@ -459,7 +459,17 @@ struct DivArgs {
   double aa, bb, cc, scale;
   int L;
   int neg;
+  int recip;
 };
+
+// v / d, or v * (1/d) for the Dirichlet (DST-I) multiplier of lid_driven_cavity.jl:17
+__device__ __forceinline__ double2 sym_apply(double2 v, double d, double sgn, bool recip) {
+  if (recip) {
+    const double id = 1.0 / d;
+    return make_double2((sgn * v.x) * id, (sgn * v.y) * id);
+  }
+  return make_double2(sgn * v.x / d, sgn * v.y / d);
+}
 
 // After the forward transform's last stage a thread holds elements (j_b + r*NS), the same
 // set the inverse transform's stage 0 reads (tid + T*r'), in a different register order:
@@ -536,8 +546,8 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
       const double d0 = fd_symbol(ax, da.cc, cyk);   // kx = eps column
       const double dL = fd_symbol(axL, da.cc, cyk);  // kx = -pi column
       const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0 (Common.jl:118)
-                                : make_double2(sgn * A.x / d0, sgn * A.y / d0);
-      const double2 B2 = make_double2(sgn * B.x / dL, sgn * B.y / dL);
+                                : sym_apply(A, d0, sgn, da.recip);
+      const double2 B2 = sym_apply(B, dL, sgn, da.recip);
       v[r] = make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
     }
   }
@@ -659,7 +669,7 @@ void launch_fused_n(int pass, const FusedPoissonArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(rows_fwd_kernel<L>, dim3(persistent_grid(a.ncu, row_per_cu, M / C::XR)),
                        dim3(C::THREADS), 0, st, a.f, a.H, M, a.twL, a.twN);
   } else if (pass == 1) {
-    DivArgs da{a.cx, a.cy, a.aa, a.bb, a.cc, a.scale, L, a.neg ? 1 : 0};
+    DivArgs da{a.cx, a.cy, a.aa, a.bb, a.cc, a.scale, L, a.neg ? 1 : 0, a.recip ? 1 : 0};
     (void)col_per_cu;
     hipLaunchKernelGGL(cols_kernel<N>, dim3(L), dim3(Plan<N>::T), 0, st, a.H, a.twN, da);
   } else {

@@ -164,7 +164,11 @@ __global__ __launch_bounds__(256) void divide_kernel(const DivideParams p) {
     }
     const double ax = p.aa + p.bb * p.cx[kx];
     const double d = ax + p.cc * p.cy[j];
-    if (p.cy_mirror == nullptr) {
+    if (p.recip) {  // iden = 1/d precomputed by the reference, then e * iden
+      const double id = 1.0 / d;
+      o.x = (v.x * id) * p.scale;
+      o.y = (v.y * id) * p.scale;
+    } else if (p.cy_mirror == nullptr) {
       o.x = (v.x / d) * p.scale;  // Julia Complex/Real: componentwise division
       o.y = (v.y / d) * p.scale;
     } else {

@@ -141,6 +141,48 @@ int cfdj_vm_set_poisson(cfdj_vm* h, int path);
 int cfdj_vm_get_poisson(cfdj_vm* h);
 void cfdj_vm_destroy(cfdj_vm* h);
 
+/* ---- lid-driven cavity: 18_NS2D_Lid_Driven_Cavity/lid_driven_cavity.jl ---------------
+ * (nx+1)-by-(ny+1) node arrays wn, sn (column-major, ld >= nx+1) on the unit box with
+ * dx = 1/nx, dy = 1/ny.  One step = the RK3 loop body of lid_driven_cavity.jl:75-114:
+ * three (rhs, stage update, bc2 Jensen wall vorticity, fps_sine DST-I Poisson) rounds and
+ * the RMS of the streamfunction change. */
+typedef struct cfdj_cavity cfdj_cavity;
+#define CFDJ_CAVITY_DST 0 /* fps_sine (lid_driven_cavity.jl:11-21), the reference's solver */
+#define CFDJ_CAVITY_MG 1  /* V-cycle multigrid (mg_N.jl), red-black GS, warm-started */
+int cfdj_cavity_create(int nx, int ny, double dx, double dy, double re, int device,
+                       cfdj_cavity** out);
+/* Poisson solver for the streamfunction; n_level/v1/v2/v3/tol/max_iter as mg_N.jl:7
+ * (ignored for CFDJ_CAVITY_DST). */
+int cfdj_cavity_set_poisson(cfdj_cavity* h, int solver, int n_level, int v1, int v2, int v3,
+                            double tol, int max_iter);
+int cfdj_cavity_upload(cfdj_cavity* h, const double* wn, long ldw, const double* sn, long lds);
+int cfdj_cavity_download(cfdj_cavity* h, double* wn, long ldw, double* sn, long lds);
+/* nsteps RK3 steps; rms[k] (may be NULL) = lid_driven_cavity.jl:112-114 of step k. */
+int cfdj_cavity_step(cfdj_cavity* h, double dt, int nsteps, double* rms);
+/* lid_driven_cavity.jl:124-159 `rhs`: r interior from w, s (r boundary left 0). */
+int cfdj_cavity_rhs(cfdj_cavity* h, const double* w, long ldw, const double* s, long lds,
+                    double* r, long ldr);
+/* Total V-cycles run by the multigrid Poisson solves so far. */
+long cfdj_cavity_mg_iterations(cfdj_cavity* h);
+void cfdj_cavity_destroy(cfdj_cavity* h);
+/* lid_driven_cavity.jl:11-21 `fps_sine`: s[2:nx,2:ny] solving the 5-point Dirichlet
+ * Poisson problem with right-hand side f[2:nx,2:ny] (one-shot). */
+int cfdj_fps_sine(int nx, int ny, double dx, double dy, const double* f, long ldf, double* s,
+                  long lds);
+
+/* ---- multigrid: 17_Poisson_Solver_Multigrid/mg_N.jl:7-114 -------------------------------
+ * n_level-level V-cycle on the (nx+1)x(ny+1) Dirichlet problem lap(u) = f; u carries the
+ * boundary values in and the solution out.  Smoother: red-black ordering of the
+ * Common.jl:78-92 Gauss-Seidel update (the reference sweeps lexicographically; converged
+ * solutions agree to the tolerance).  rms_hist (may be NULL) receives iterations+1
+ * residual norms (Common.jl:229-232), the first being the initial residual. */
+typedef struct cfdj_mg cfdj_mg;
+int cfdj_mg_create(int nx, int ny, double dx, double dy, int n_level, int v1, int v2, int v3,
+                   int device, cfdj_mg** out);
+int cfdj_mg_solve(cfdj_mg* h, const double* f, long ldf, double* u, long ldu, double tol,
+                  int max_iter, int* iterations, double* rms_hist);
+void cfdj_mg_destroy(cfdj_mg* h);
+
 #ifdef __cplusplus
 }
 #endif

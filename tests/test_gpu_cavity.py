@@ -1,0 +1,112 @@
+"""GPU parity of the secondary paths: lid-driven cavity and multigrid.
+
+Tolerances: cavity rhs bit-exact given (w, s); fps_sine within 1e-12 max|s| (DST via the
+odd-extension FFT vs scipy's DST-I); cavity fields after K steps within 1e-10; multigrid:
+red-black vs the reference's lexicographic smoother -> converged solutions compared at the
+solver tolerance, and the ipr=1 MMS (exact for the 5-point Laplacian) to ~1e-8.
+"""
+import numpy as np
+import pytest
+
+from oracle import cavity_oracle as co
+from tests.golden.make_golden import smooth_field
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from cfd_julia_amd import _lib
+
+    assert _lib.require_gpu() >= 1
+    return _lib
+
+
+@pytest.mark.parametrize("n", [16, 64, 96])
+def test_gpu_cavity_rhs_bit_exact(lib, n):
+    from cfd_julia_amd.cavity import Cavity
+
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    w = np.asfortranarray(np.pad(smooth_field(n - 1, n - 1, 3, 61), ((1, 1), (1, 1)))[:n + 1, :n + 1])
+    s = np.asfortranarray(np.pad(smooth_field(n - 1, n - 1, 3, 62), ((1, 1), (1, 1)))[:n + 1, :n + 1])
+    with Cavity(n, n, dx, dy, 100.0) as h:
+        r = h.rhs(w, s)
+    ref = co.cavity_rhs(w, s, dx, dy, 100.0)
+    assert np.array_equal(r, ref)
+
+
+@pytest.mark.parametrize("n", [16, 64, 512, 1024])
+def test_gpu_fps_sine_vs_oracle(lib, n):
+    from cfd_julia_amd.cavity import fps_sine
+
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    f = np.zeros((n + 1, n + 1), order="F")
+    f[1:n, 1:n] = smooth_field(n - 1, n - 1, 4, 63)
+    s = fps_sine(n, n, dx, dy, f)
+    ref = co.fps_sine(f, dx, dy)
+    assert np.all(s[0, :] == 0) and np.all(s[:, 0] == 0) and np.all(s[n, :] == 0)
+    assert np.abs(s - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("n,nt", [(32, 50), (64, 20), (512, 3)])
+def test_gpu_cavity_steps_vs_oracle(lib, n, nt):
+    from cfd_julia_amd import cavity
+
+    dt = 0.001 * (64 / n) ** 2
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    wn = np.zeros((n + 1, n + 1), order="F")
+    sn = np.zeros((n + 1, n + 1), order="F")
+    rms = np.zeros(nt)
+    cavity.numerical(n, n, nt, dx, dy, dt, 100.0, wn, sn, rms)
+    w_ref, s_ref, rms_ref = co.cavity_numerical(n, n, nt, dt, 100.0)
+    assert np.abs(wn - w_ref).max() < 1e-10 * max(1.0, np.abs(w_ref).max())
+    assert np.abs(sn - s_ref).max() < 1e-12
+    assert np.allclose(rms, rms_ref, rtol=1e-8, atol=1e-16)
+
+
+def test_gpu_cavity_mg_matches_dst(lib):
+    from cfd_julia_amd.cavity import Cavity
+
+    n, nt, dt = 64, 20, 0.001
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    out = {}
+    for p in ("dst", "mg"):
+        with Cavity(n, n, dx, dy, 100.0, poisson=p, tol=1e-12) as h:
+            rms = h.step(dt, nt)
+            out[p] = h.download() + (rms, h.mg_iterations() if p == "mg" else 0)
+    (w1, s1, r1, _), (w2, s2, r2, its) = out["dst"], out["mg"]
+    assert its > 0
+    assert np.abs(s1 - s2).max() < 1e-9 * np.abs(s1).max()
+    assert np.abs(w1 - w2).max() < 1e-6 * np.abs(w1).max()
+
+
+@pytest.mark.parametrize("n,levels", [(64, 5), (512, 9)])
+def test_gpu_mg_mms(lib, n, levels):
+    from cfd_julia_amd import mg
+
+    f, ue, un, dx, dy = mg.mms(n)
+    it, hist = mg.mg_N(dx, dy, n, n, None, f, un, 2, 2, 2, 100000, 1e-9, n_level=levels)
+    assert hist[-1] / hist[0] <= 1e-9 and it < 50
+    # ipr = 1: (x^2-1)(y^2-1) is exact for the 5-point Laplacian -> solver error only
+    assert np.abs(un - ue).max() < 1e-7
+    # the red-black GPU V-cycle vs the oracle's red-black restatement: same iterations,
+    # residual histories equal to round-off
+    if n <= 64:
+        u0 = mg.mms(n)[2]
+        u_o, it_o, hist_o = co.mg_n(f, u0, dx, dy, levels)
+        assert it == it_o
+        np.testing.assert_allclose(hist, hist_o, rtol=1e-9)
+        assert np.abs(un - u_o).max() < 1e-12
+
+
+def test_gpu_mg_vs_reference_lexicographic(lib):
+    """Reference smoother (lexicographic GS) vs the GPU's red-black: different iterates,
+    same converged solution to the tolerance."""
+    from cfd_julia_amd import mg
+
+    n, levels = 32, 4
+    f, ue, un, dx, dy = mg.mms(n, ipr=2)
+    mg.mg_N(dx, dy, n, n, None, f, un, 2, 2, 2, 100000, 1e-10, n_level=levels)
+    u_lex, it_lex, _ = co.mg_n(f, mg.mms(n, ipr=2)[2], dx, dy, levels, tol=1e-10,
+                               smoother=co.gauss_seidel_lex)
+    assert np.abs(un - u_lex).max() < 1e-9 * np.abs(u_lex).max()
