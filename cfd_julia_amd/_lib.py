@@ -97,6 +97,9 @@ SIGNATURES = {
     "cfdj_mg_solve": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long, C.c_double, C.c_int, _ip,
                                 _dp]),
     "cfdj_mg_destroy": (None, [_vp]),
+    "cfdj_jacobi_solve": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, _dp, C.c_long,
+                                    _dp, C.c_long, C.c_long, C.c_double, C.c_long, _lp, _dp]),
+    "cfdj_ftcs": (C.c_int, [C.c_int, C.c_int, C.c_double, _dp, _dp, C.c_long]),
 }
 
 _lock = threading.Lock()

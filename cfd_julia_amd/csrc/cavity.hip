@@ -227,6 +227,25 @@ __global__ __launch_bounds__(kBX* kBY) void prolong_add_kernel(const double* __r
   uf[(size_t)J * Pf + I] += p;
 }
 
+// 15_Poisson_Solver_Gauss_Seidel/gauss_seidel.jl:33-39 (a Jacobi sweep despite the name):
+// r = f - lap(u_old) everywhere, then u += r / dd -- ping-pong buffers, same expressions.
+__global__ __launch_bounds__(kBX* kBY) void jacobi_kernel(const double* __restrict__ f,
+                                                          const double* __restrict__ u,
+                                                          double* __restrict__ un,
+                                                          double* __restrict__ r, int nx,
+                                                          int ny, int P, double dx2, double dy2,
+                                                          double dd) {
+  const int i = 1 + blockIdx.x * kBX + threadIdx.x;
+  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
+  if (i >= nx || j >= ny) return;
+  const size_t c = (size_t)j * P + i;
+  const double uc = u[c];
+  const double rc = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 +
+                            (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
+  r[c] = rc;
+  un[c] = uc + rc / dd;
+}
+
 __global__ __launch_bounds__(256) void negate_kernel(const double* __restrict__ a,
                                                      double* __restrict__ b, size_t n) {
   const size_t e = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
@@ -719,6 +738,71 @@ int cfdj_mg_solve(cfdj_mg* h, const double* f, long ldf, double* u, long ldu, do
     CFDJ_HIP(hipStreamSynchronize(h->stream));
     if (iterations) *iterations = it;
     if (rms_hist) std::memcpy(rms_hist, hist.data(), hist.size() * sizeof(double));
+  });
+}
+
+int cfdj_jacobi_solve(int nx, int ny, double dx, double dy, const double* f, long ldf,
+                      double* u, long ldu, long max_iter, double tol, long freq,
+                      long* iterations, double* rms_out) {
+  return guard([&] {
+    CFDJ_REQUIRE(f && u && ldf >= nx + 1 && ldu >= nx + 1, "bad f / u");
+    CFDJ_REQUIRE(nx >= 2 && ny >= 2 && dx > 0 && dy > 0 && freq >= 1 && max_iter >= 0,
+                 "bad arguments");
+    hipStream_t st = nullptr;
+    CFDJ_HIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    const int P = nx + 2;
+    const size_t n = (size_t)P * (ny + 1);
+    double *df = nullptr, *ua = nullptr, *ub = nullptr, *r = nullptr, *part = nullptr,
+           *d_rms = nullptr;
+    struct Free {
+      std::vector<double**> ps;
+      hipStream_t st;
+      ~Free() {
+        for (auto p : ps) dfree(*p);
+        if (st) (void)hipStreamDestroy(st);
+      }
+    } fr{{&df, &ua, &ub, &r, &part, &d_rms}, st};
+    df = dalloc<double>(n);
+    ua = dalloc<double>(n);
+    ub = dalloc<double>(n);
+    r = dalloc<double>(n);
+    part = dalloc<double>(512);
+    d_rms = dalloc<double>(1);
+    CFDJ_HIP(hipMemsetAsync(r, 0, n * sizeof(double), st));
+    copy_in(df, P, f, ldf, nx, ny, st);
+    copy_in(ua, P, u, ldu, nx, ny, st);
+    CFDJ_HIP(hipMemcpyAsync(ub, ua, n * sizeof(double), hipMemcpyDeviceToDevice, st));
+    const double dx2 = dx * dx, dy2 = dy * dy, dd = -2.0 / dx2 - 2.0 / dy2;
+    auto rms_now = [&](const double* uu) {  // compute_residual + compute_l2norm
+      hipLaunchKernelGGL(residual_kernel, interior_grid(nx, ny), dim3(kBX, kBY), 0, st, df, uu,
+                         r, nx, ny, P, dx2, dy2);
+      launch_rms(r, nullptr, 1, nx - 1, 1, ny - 1, P, (double)(nx - 1) * (ny - 1), part, 512,
+                 d_rms, st);
+      double h = 0.0;
+      CFDJ_HIP(hipMemcpyAsync(&h, d_rms, sizeof(double), hipMemcpyDeviceToHost, st));
+      CFDJ_HIP(hipStreamSynchronize(st));
+      return h;
+    };
+    const double init_rms = rms_now(ua);
+    double rms = init_rms;
+    long it = 0;
+    double* cur = ua;
+    double* nxt = ub;
+    while (it < 5 * max_iter) {  // gauss_seidel.jl:19
+      ++it;
+      hipLaunchKernelGGL(jacobi_kernel, interior_grid(nx, ny), dim3(kBX, kBY), 0, st, df, cur,
+                         nxt, r, nx, ny, P, dx2, dy2, dd);
+      std::swap(cur, nxt);
+      if (it % freq == 0) {
+        rms = rms_now(cur);
+        if (rms / init_rms <= tol) break;
+      }
+    }
+    CFDJ_HIP(hipGetLastError());
+    copy_out(u, ldu, cur, P, nx, ny, st);
+    CFDJ_HIP(hipStreamSynchronize(st));
+    if (iterations) *iterations = it;
+    if (rms_out) *rms_out = rms;
   });
 }
 

@@ -503,6 +503,21 @@ extern "C" {
 
 const char* cfdj_last_error(void) { return g_err.c_str(); }
 
+// 01_Heat_Equation_FTCS/ftcs.jl:34-41 -- host code (BASELINE config 1 is CPU plumbing only).
+int cfdj_ftcs(int nx, int nt, double beta, const double* u0, double* un, long ldu) {
+  return guard([&] {
+    CFDJ_REQUIRE(nx >= 2 && nt >= 0 && u0 && un && ldu >= nx + 1, "bad arguments");
+    for (int i = 0; i <= nx; ++i) un[i] = u0[i];
+    for (int k = 1; k <= nt; ++k) {
+      const double* a = un + (size_t)(k - 1) * ldu;
+      double* b = un + (size_t)k * ldu;
+      for (int i = 1; i < nx; ++i) b[i] = a[i] + beta * (a[i + 1] - 2.0 * a[i] + a[i - 1]);
+      b[0] = 0.0;   // boundary condition at x = -1 (ftcs.jl:39)
+      b[nx] = 0.0;  // boundary condition at x = 1 (ftcs.jl:40)
+    }
+  });
+}
+
 const char* cfdj_version(void) { return "cfdj 0.1.0 (gfx950)"; }
 
 int cfdj_device_count(void) {

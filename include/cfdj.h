@@ -183,6 +183,19 @@ int cfdj_mg_solve(cfdj_mg* h, const double* f, long ldf, double* u, long ldu, do
                   int max_iter, int* iterations, double* rms_hist);
 void cfdj_mg_destroy(cfdj_mg* h);
 
+/* ---- 15_Poisson_Solver_Gauss_Seidel/gauss_seidel.jl:8-54 ----------------------------------
+ * The reference's "Gauss-Seidel" is a Jacobi sweep (residual of the old iterate everywhere,
+ * then u += r / (-2/dx^2 - 2/dy^2)); up to 5*max_iter sweeps, convergence checked every
+ * freq sweeps against tol * the initial residual norm.  u in/out (boundary = data). */
+int cfdj_jacobi_solve(int nx, int ny, double dx, double dy, const double* f, long ldf,
+                      double* u, long ldu, long max_iter, double tol, long freq,
+                      long* iterations, double* rms);
+
+/* ---- 01_Heat_Equation_FTCS/ftcs.jl:34-41 (host code: BASELINE config 1 is CPU-only) -------
+ * un is (nx+1) x (nt+1) column-major (ld >= nx+1): column 0 is u0, column k the FTCS step
+ * u_i <- u_i + beta (u_{i+1} - 2 u_i + u_{i-1}) with u_0 = u_nx = 0. */
+int cfdj_ftcs(int nx, int nt, double beta, const double* u0, double* un, long ldu);
+
 #ifdef __cplusplus
 }
 #endif

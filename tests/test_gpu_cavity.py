@@ -110,3 +110,27 @@ def test_gpu_mg_vs_reference_lexicographic(lib):
     u_lex, it_lex, _ = co.mg_n(f, mg.mms(n, ipr=2)[2], dx, dy, levels, tol=1e-10,
                                smoother=co.gauss_seidel_lex)
     assert np.abs(un - u_lex).max() < 1e-9 * np.abs(u_lex).max()
+
+
+# ---- 15_Poisson_Solver_Gauss_Seidel/gauss_seidel.jl (a Jacobi sweep) ---------------------
+def test_gpu_jacobi_bit_exact_fixed_sweeps(lib):
+    from cfd_julia_amd.gauss_seidel import gauss_seidel
+    from oracle import misc_oracle as mo
+
+    n = 64
+    f, ue, un, dx, dy = co.mg_mms(n, ipr=2)
+    u = np.asfortranarray(un.copy())
+    it, _ = gauss_seidel(dx, dy, n, n, None, f, u, 60, 0.0, freq=1000)  # tol 0: 300 sweeps
+    u_ref, it_ref, _ = mo.gauss_seidel(f, un.copy(), dx, dy, 60, 0.0, freq=1000)
+    assert it == it_ref == 300
+    assert np.array_equal(u, u_ref)
+
+
+def test_gpu_jacobi_converges_mms(lib):
+    from cfd_julia_amd.gauss_seidel import gauss_seidel
+
+    n = 32
+    f, ue, un, dx, dy = co.mg_mms(n, ipr=1)
+    u = np.asfortranarray(un.copy())
+    it, rms = gauss_seidel(dx, dy, n, n, None, f, u, 20000, 1e-9, freq=100)
+    assert it < 5 * 20000 and np.abs(u - ue).max() < 1e-7

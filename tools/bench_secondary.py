@@ -1,0 +1,78 @@
+"""Secondary BASELINE configs (not the headline bench line):
+
+  C2  2D FFT Poisson (12/fft_p.jl) 2048^2 periodic: GPU solve time (device-resident, fused
+      3-pass path) vs the CPU oracle (scipy.fft, all host cores), with the MMS L2 error.
+  C4  lid-driven cavity (18/lid_driven_cavity.jl) 2048^2, re = 100, dt = 5e-6: ms per RK3
+      step with the DST-I (fused FFT on the 4096^2 odd extension) and the V-cycle MG solver.
+
+  python tools/bench_secondary.py [--steps 20]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+
+
+def bench_poisson(n=2048, reps=20):
+    import torch
+
+    from cfd_julia_amd import PoissonFFT, fft_p
+    from oracle import vm_oracle as vo
+
+    f, ue, dx, dy = fft_p.mms(n)
+    out = {"config": f"C2 fft_p {n}^2"}
+    with PoissonFFT(n, n, dx, dy) as h:
+        fd = torch.tensor(np.ascontiguousarray(f[:n, :n].T), dtype=torch.float64, device="cuda")
+        sd = torch.empty_like(fd)
+        for path in ("fused", "rocfft"):
+            h.set_poisson(path)
+            h.solve_device(fd.data_ptr(), sd.data_ptr())
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                h.solve_device(fd.data_ptr(), sd.data_ptr())
+            torch.cuda.synchronize()
+            out[f"gpu_{path}_ms"] = round((time.perf_counter() - t0) * 1e3 / reps, 4)
+        un = np.zeros_like(f)
+        un[:n, :n] = sd.cpu().numpy().T
+    un[n, :] = un[0, :]
+    un[:, n] = un[:, 0]
+    out["l2_error"] = float(np.sqrt(np.mean((un - ue) ** 2)))
+    workers = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    t0 = time.perf_counter()
+    vo.ps_fft(np.ascontiguousarray(f[:n, :n]), dx, dy, workers=workers)
+    out["cpu_oracle_ms"] = round((time.perf_counter() - t0) * 1e3, 2)
+    out["cpu_workers"] = workers
+    return out
+
+
+def bench_cavity(n=2048, steps=20, dt=5e-6):
+    from cfd_julia_amd.cavity import Cavity
+
+    out = {"config": f"C4 cavity {n}^2 re=100 dt={dt}"}
+    dx = 1.0 / n
+    for p in ("dst", "mg"):
+        with Cavity(n, n, dx, dx, 100.0, poisson=p, tol=1e-6) as h:
+            h.step(dt, 2)
+            t0 = time.perf_counter()
+            rms = h.step(dt, steps)
+            t = time.perf_counter() - t0
+            out[f"{p}_ms_per_step"] = round(t * 1e3 / steps, 3)
+            out[f"{p}_MLUPS"] = round(n * n * steps / t / 1e6, 1)
+            out[f"{p}_final_rms"] = float(rms[-1])
+            if p == "mg":
+                out["mg_vcycles_total"] = int(h.mg_iterations())
+    return out
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--steps", type=int, default=20)
+    a = ap.parse_args()
+    print(json.dumps(bench_poisson()))
+    print(json.dumps(bench_cavity(steps=a.steps)))
