@@ -78,6 +78,7 @@ SIGNATURES = {
     "cfdj_vm_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_get_poisson": (C.c_int, [_vp]),
     "cfdj_fps_set_poisson": (C.c_int, [_vp, C.c_int]),
+    "cfdj_fps_get_poisson": (C.c_int, [_vp]),
     "cfdj_fps_set_symbol": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_destroy": (None, [_vp]),
     "cfdj_cavity_create": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,

@@ -574,8 +574,8 @@ int cfdj_cavity_create(int nx, int ny, double dx, double dy, double re, int devi
     h->sym.init(NX, NY, dx, dy, 0.0, kSymbolDirichletExt);
     h->ext = dalloc<double>((size_t)NX * NY);
     h->spec = dalloc<double2>((size_t)(NX / 2 + 1) * NY);
-    if (fused_poisson_supported(NX, NY)) {
-      h->fused.init(NX);
+    if (fused_ok(NX, NY, 1)) {
+      h->fused.init(NX, NY);
       h->use_fused = true;
     } else {
       size_t lens[2] = {(size_t)NX, (size_t)NY};

@@ -215,6 +215,34 @@ struct cfdj_vm {
       }
       return;
     }
+    if (use_fused) {
+      // y-slabs, hand-written passes: row r2c writes the column-major half spectrum X,
+      // whose column blocks ARE the all-to-all chunks (no pack); the receive buffer Y holds
+      // this rank's columns as P row segments, which the column pass addresses directly.
+      const size_t cnt = (size_t)(nx / 2 / nranks) * rows;
+      std::vector<FusedPoissonArgs> a;
+      for (size_t i = 0; i < slabs.size(); ++i)
+        a.push_back(fused.args(sym, src[i], slabs[i].psi, slabs[i].X, slabs[i].Y, rows,
+                               slabs[i].rank, nranks, neg));
+      for (auto& ai : a) {
+        tbegin(CFDJ_K_FFT_FWD);
+        launch_fused_poisson_pass(0, ai, stream);
+        tend();
+      }
+      alltoall([](Slab& s, bool send) { return send ? s.X : s.Y; }, cnt);
+      for (auto& ai : a) {
+        tbegin(CFDJ_K_DIVIDE);
+        launch_fused_poisson_pass(1, ai, stream);
+        tend();
+      }
+      alltoall([](Slab& s, bool send) { return send ? s.Y : s.X; }, cnt);
+      for (auto& ai : a) {
+        tbegin(CFDJ_K_FFT_INV);
+        launch_fused_poisson_pass(2, ai, stream);
+        tend();
+      }
+      return;
+    }
     if (!slab_mode()) {
       Slab& s = slabs[0];
       tbegin(CFDJ_K_FFT_FWD);
@@ -421,8 +449,8 @@ struct cfdj_vm {
     }
     plans.finalize(stream);
     d_flag = dalloc<int>(1);
-    if (!slab_mode() && fused_poisson_supported(nx, ny)) {
-      fused.init(nx);
+    if (fused_ok(nx, ny, nranks)) {
+      fused.init(nx, ny);
       use_fused = true;
     }
   }
@@ -551,8 +579,8 @@ int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device
     h->spec = dalloc<double2>((size_t)h->sym.nxh * ny);
     h->f_dev = dalloc<double>((size_t)nx * ny);
     h->s_dev = dalloc<double>((size_t)nx * ny);
-    if (fused_poisson_supported(nx, ny)) {
-      h->fused.init(nx);
+    if (fused_ok(nx, ny, 1)) {
+      h->fused.init(nx, ny);
       h->use_fused = true;
     }
     *out = h.release();
@@ -805,8 +833,8 @@ int cfdj_vm_set_poisson(cfdj_vm* h, int path) {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
     CFDJ_REQUIRE(path >= CFDJ_POISSON_AUTO && path <= CFDJ_POISSON_FUSED, "bad path");
     select_device(h->device);
-    const bool f = resolve_fused(path, h->nx, h->ny, h->slab_mode());
-    if (f && !h->fused.twN) h->fused.init(h->nx);
+    const bool f = resolve_fused(path, h->nx, h->ny, h->nranks);
+    if (f && !h->fused.ready()) h->fused.init(h->nx, h->ny);
     h->use_fused = f;
     h->invalidate_graph();
   });
@@ -823,6 +851,11 @@ int cfdj_vm_set_graph(cfdj_vm* h, int enable) {
 }
 
 int cfdj_vm_get_poisson(cfdj_vm* h) {
+  if (!h) return CFDJ_ERR_ARG;
+  return h->use_fused ? CFDJ_POISSON_FUSED : CFDJ_POISSON_ROCFFT;
+}
+
+int cfdj_fps_get_poisson(cfdj_fps_plan* h) {
   if (!h) return CFDJ_ERR_ARG;
   return h->use_fused ? CFDJ_POISSON_FUSED : CFDJ_POISSON_ROCFFT;
 }
@@ -844,8 +877,8 @@ int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path) {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
     CFDJ_REQUIRE(path >= CFDJ_POISSON_AUTO && path <= CFDJ_POISSON_FUSED, "bad path");
     select_device(h->device);
-    const bool f = resolve_fused(path, h->sym.nx, h->sym.ny, false);
-    if (f && !h->fused.twN) h->fused.init(h->sym.nx);
+    const bool f = resolve_fused(path, h->sym.nx, h->sym.ny, 1);
+    if (f && !h->fused.ready()) h->fused.init(h->sym.nx, h->sym.ny);
     h->use_fused = f;
   });
 }

@@ -117,24 +117,33 @@ void launch_pack(const double2* X, double2* S, int nxh, int rows, int kb, int nr
 void launch_unpack(const double2* S, double2* X, int nxh, int rows, int kb, int nranks,
                    hipStream_t st);
 
-// Hand-written fused FD-FFT Poisson for square power-of-two grids (poisson_fft.hip):
-// pass 0 = row r2c (f -> column-tiled packed half spectrum H), pass 1 = per-tile column
-// FFT + divide + inverse FFT (in place on H), pass 2 = row c2r (H -> s).
+// Hand-written fused FD-FFT Poisson for power-of-two grids (poisson_fft.hip):
+// pass 0 = row r2c (f -> column-major packed half spectrum H[m][y], pitch `rows`),
+// pass 1 = column FFT + divide + inverse FFT on C (in place), pass 2 = row c2r (H -> s).
+// One GPU: C == H.  y-slabs: H is the all-to-all send buffer (columns [q kb, (q+1) kb) are
+// the contiguous chunk for rank q), C the receive buffer, where column ml of this rank is
+// stored as P segments of `rows` elements (one per source rank), kb * rows apart.
 struct FusedPoissonArgs {
-  int n;                // nx == ny
-  const double* f;      // input field (pitch n)
-  double* s;            // output streamfunction (pitch n)
-  double2* H;           // (n/2) x n complex work spectrum
-  const double2* twL;   // exp(-2 pi i k/(n/2)), k < n/2
-  const double2* twN;   // exp(-2 pi i k/n), k < n
-  const double* cx;     // cos(kx[m]), m <= n/2
-  const double* cy;     // cos(ky[k]), k < n
+  int nx, ny, rows;     // row length, column length (global ny), rows of this GPU
+  const double* f;      // input field (pitch nx, `rows` rows)
+  double* s;            // output streamfunction (pitch nx)
+  double2* H;           // (nx/2) x rows packed half spectrum, column-major
+  double2* C;           // column-pass buffer (kb columns of ny)
+  int m0, kb;           // first global column and column count of C
+  int rl_log2;          // log2(rows per column segment of C)
+  unsigned seg;         // elements between the segments of one column of C
+  const double2* twL;   // exp(-2 pi i k/(nx/2)), k < nx/2
+  const double2* twN;   // exp(-2 pi i k/nx), k < nx
+  const double2* twM;   // exp(-2 pi i k/ny), k < ny
+  const double* cx;     // cos(kx[m]), m <= nx/2
+  const double* cy;     // cos(ky[k]), k < ny
+  const double* cy_mirror;  // cy[(ny-k) % ny] or nullptr (symbol even in ky)
   double aa, bb, cc, scale;
   bool neg;
   bool recip;           // see DivideParams::recip
   int ncu;              // compute units (persistent grid size)
 };
-bool fused_poisson_supported(int nx, int ny);
+bool fused_poisson_supported(int nx, int ny, int rows);
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);
 
 // Finiteness check: sets *flag = 1 if any element is not finite.

@@ -233,32 +233,50 @@ inline double2* twiddle_table(int n) {
 
 // Hand-written 3-pass FFT Poisson (poisson_fft.hip) state: twiddle tables.
 struct Fused {
-  int n = 0, ncu = 256;
+  int nx = 0, ny = 0, ncu = 256;
   double2* twL = nullptr;
   double2* twN = nullptr;
-  void init(int n_) {
-    n = n_;
+  double2* twM = nullptr;  // == twN on square grids
+  bool ready() const { return twN != nullptr; }
+  void init(int nx_, int ny_) {
+    nx = nx_;
+    ny = ny_;
     int dev = 0;
     CFDJ_HIP(hipGetDevice(&dev));
     CFDJ_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-    twL = twiddle_table(n / 2);
-    twN = twiddle_table(n);
+    twL = twiddle_table(nx / 2);
+    twN = twiddle_table(nx);
+    twM = ny == nx ? twN : twiddle_table(ny);
   }
   void destroy() {
+    if (twM != twN) dfree(twM);
     dfree(twL);
     dfree(twN);
+    twL = twN = twM = nullptr;
   }
-  FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H,
-                        bool neg) const {
+  // y-slab `rank` of `nranks` (rows = ny / nranks); one GPU: rank 0 of 1, C == H.
+  FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H, double2* C,
+                        int rows, int rank, int nranks, bool neg) const {
     FusedPoissonArgs a;
-    a.n = n;
+    a.nx = nx;
+    a.ny = ny;
+    a.rows = rows;
     a.f = f;
     a.s = s;
     a.H = H;
+    a.C = C;
+    a.kb = (nx / 2) / nranks;
+    a.m0 = rank * a.kb;
+    int lg = 0;
+    while ((1 << lg) < rows) ++lg;
+    a.rl_log2 = lg;
+    a.seg = (unsigned)((size_t)a.kb * rows);
     a.twL = twL;
     a.twN = twN;
+    a.twM = twM;
     a.cx = sym.cx;
     a.cy = sym.cy;
+    a.cy_mirror = sym.cy_mirror;
     a.aa = sym.aa;
     a.bb = sym.bb;
     a.cc = sym.cc;
@@ -268,15 +286,26 @@ struct Fused {
     a.ncu = ncu;
     return a;
   }
+  FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H,
+                        bool neg) const {
+    return args(sym, f, s, H, H, ny, 0, 1, neg);
+  }
 };
 
+// The fused path on `nranks` y-slabs: power-of-two slabs whose column blocks split evenly.
+inline bool fused_ok(int nx, int ny, int nranks) {
+  if (nranks < 1 || (nranks & (nranks - 1)) != 0 || ny % nranks != 0) return false;
+  if ((nx / 2) % nranks != 0) return false;
+  return fused_poisson_supported(nx, ny, ny / nranks);
+}
+
 // Poisson path selection (cfdj_vm_set_poisson / cfdj_fps_set_poisson).
-inline bool resolve_fused(int path, int nx, int ny, bool slab) {
+inline bool resolve_fused(int path, int nx, int ny, int nranks) {
   if (path == CFDJ_POISSON_ROCFFT) return false;
-  const bool ok = !slab && fused_poisson_supported(nx, ny);
+  const bool ok = fused_ok(nx, ny, nranks);
   if (path == CFDJ_POISSON_FUSED && !ok)
-    throw Error{CFDJ_ERR_ARG, "fused Poisson needs a single-GPU square grid of 1024, 2048 "
-                              "or 4096 points per side"};
+    throw Error{CFDJ_ERR_ARG, "fused Poisson needs power-of-two sides, nx 1024..16384, ny "
+                              "1024..8192, a power-of-two rank count and >= 8 rows per rank"};
   return ok;
 }
 

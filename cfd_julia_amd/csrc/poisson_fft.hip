@@ -359,7 +359,12 @@ __device__ __forceinline__ Range persistent_range(int b, int nb, int n) {
 template <int L>
 struct RowCfg {
   static constexpr int T = Plan<L>::T;
-  static constexpr int XR = (256 / T) > 4 ? (256 / T) : 4;  // rows per work item
+  // rows per work item: >= 4 (64-B column segments) where the LDS holds them, fewer for
+  // the long rows of the multi-GPU grids (L = 4096: 2, L = 8192: 1 -- 136 KB per row)
+  static constexpr int XR_WANT = (256 / T) > 4 ? (256 / T) : 4;
+  static constexpr int XR_FIT = (140 * 1024) / (Plan<L>::ROWSTRIDE * 16);
+  static constexpr int XR = XR_WANT < XR_FIT ? XR_WANT : XR_FIT;
+  static_assert(XR >= 1, "row does not fit the LDS");
   static constexpr int THREADS = XR * T;
   static constexpr int PAIRS = (L / 2) * XR / THREADS;  // (m, L-m) pairs per thread
 };
@@ -454,21 +459,31 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
 // Pass 2: one column at a time: forward FFT, divide, inverse FFT, in place.
 // ---------------------------------------------------------------------------------------
 struct DivArgs {
-  const double* cx;  // cos(kx[m]), m <= L
-  const double* cy;  // cos(ky[k]), k < M
+  const double* cx;         // cos(kx[m]), m <= L (global m)
+  const double* cy;         // cos(ky[k]), k < M
+  const double* cy_mirror;  // cy[(M - k) % M] when the symbol is not even in ky (ny < nx)
   double aa, bb, cc, scale;
   int L;
   int neg;
   int recip;
+  int m0;         // global index of this buffer's first column (y-slabs: rank * L/P)
+  int rl_log2;    // rows per segment (y-slabs: rows per rank; one GPU: M)
+  unsigned seg;   // elements between the segments of one column (y-slabs: (L/P) * rows)
 };
 
-// v / d, or v * (1/d) for the Dirichlet (DST-I) multiplier of lid_driven_cavity.jl:17
-__device__ __forceinline__ double2 sym_apply(double2 v, double d, double sgn, bool recip) {
+// v / d, or v * (1/d) for the Dirichlet (DST-I) multiplier of lid_driven_cavity.jl:17, or
+// the Hermitian projection (v/d + v/d2)/2 of a symbol that is not even in ky: what
+// real(ifft(...)) keeps of a non-Hermitian quotient (Common.jl:123 with ny < nx).  The
+// sign is applied first, as divide_kernel does.
+__device__ __forceinline__ double2 sym_apply(double2 v, double d, double d2, double sgn,
+                                             bool recip, bool mirror) {
+  const double x = sgn * v.x, y = sgn * v.y;
   if (recip) {
     const double id = 1.0 / d;
-    return make_double2((sgn * v.x) * id, (sgn * v.y) * id);
+    return make_double2(x * id, y * id);
   }
-  return make_double2(sgn * v.x / d, sgn * v.y / d);
+  if (mirror) return make_double2(0.5 * (x / d + x / d2), 0.5 * (y / d + y / d2));
+  return make_double2(x / d, y / d);
 }
 
 // After the forward transform's last stage a thread holds elements (j_b + r*NS), the same
@@ -484,33 +499,41 @@ __device__ __forceinline__ void fwd_to_inv(const double2 (&a)[16], double2 (&v)[
     for (int r = 0; r < RL; ++r) v[b + (16 / RL) * r] = a[b * RL + r];
 }
 
+// Element y of a column: rows are stored in segments of 2^rl_log2 (one per source rank of
+// the y-slab all-to-all), `seg` elements apart; on one GPU the column is one segment.
+__device__ __forceinline__ unsigned col_off(int y, int rl_log2, unsigned seg) {
+  return (unsigned)(y >> rl_log2) * seg + (unsigned)(y & ((1 << rl_log2) - 1));
+}
+
 template <int M>
 __device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __restrict__ col,
-                                         int tid) {
+                                         int tid, int rl_log2, unsigned seg) {
   constexpr int R0 = Plan<M>::radix(0);
 #pragma unroll
   for (int b = 0; b < 16 / R0; ++b)
 #pragma unroll
-    for (int r = 0; r < R0; ++r) a[b * R0 + r] = col[(unsigned)in_pos<M, 0>(tid, b, r)];
+    for (int r = 0; r < R0; ++r) a[b * R0 + r] = col[col_off(in_pos<M, 0>(tid, b, r), rl_log2, seg)];
 }
 
 template <int M>
-__global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ H,
+__global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ C,
                                                         const double2* __restrict__ twM_,
                                                         const DivArgs da) {
-  // One column per workgroup (2 resident per CU): not persistent, because the divide's
-  // cy[k] loads would queue behind a next-column prefetch (vmcnt is in order).
+  // One column per workgroup (2 resident per CU at M = 4096): not persistent, because the
+  // divide's cy[k] loads would queue behind a next-column prefetch (vmcnt is in order).
   using P = Plan<M>;
   static_assert(P::NSTAGES >= 2, "column length");
   __shared__ double2 lds[P::PAD];
   const TwGlobal<M> twM{twM_};
   const int tid = threadIdx.x;
-  const int m = xcd_remap(blockIdx.x, gridDim.x);
+  const int ml = xcd_remap(blockIdx.x, gridDim.x);
+  const int m = da.m0 + ml;  // global x-mode
   const double sgn = da.neg ? -1.0 : 1.0;
-  double2* col = H + (size_t)m * M;
+  const bool mirror = da.cy_mirror != nullptr;
+  double2* col = C + ((size_t)ml << da.rl_log2);
 
   double2 a[16];
-  load_col<M>(a, col, tid);
+  load_col<M>(a, col, tid, da.rl_log2, da.seg);
   stage_regs<M, 0, -1>(a, tid, twM);
   lds_write<M, 0>(lds, a, tid);
   __syncthreads();
@@ -524,7 +547,9 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
     for (int r = 0; r < 16; ++r) {
       const int k = tid + P::T * r;
       const double d = fd_symbol(ax, da.cc, da.cy[k]);
-      v[r] = make_double2((sgn * v[r].x / d) * da.scale, (sgn * v[r].y / d) * da.scale);
+      const double d2 = mirror ? fd_symbol(ax, da.cc, da.cy_mirror[k]) : d;
+      const double2 q = sym_apply(v[r], d, d2, sgn, da.recip, mirror);
+      v[r] = make_double2(q.x * da.scale, q.y * da.scale);
     }
   } else {
     // packed column: Z = FFT_y(X_dc + i X_nyq); split with Z[-k], divide each half by its
@@ -543,11 +568,14 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
       const double2 D = csub(Z, Zc);
       const double2 B = make_double2(0.5 * D.y, -0.5 * D.x);
       const double cyk = da.cy[k];
+      const double cym = mirror ? da.cy_mirror[k] : cyk;
       const double d0 = fd_symbol(ax, da.cc, cyk);   // kx = eps column
       const double dL = fd_symbol(axL, da.cc, cyk);  // kx = -pi column
+      const double d0m = fd_symbol(ax, da.cc, cym);
+      const double dLm = fd_symbol(axL, da.cc, cym);
       const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0 (Common.jl:118)
-                                : sym_apply(A, d0, sgn, da.recip);
-      const double2 B2 = sym_apply(B, dL, sgn, da.recip);
+                                : sym_apply(A, d0, d0m, sgn, da.recip, mirror);
+      const double2 B2 = sym_apply(B, dL, dLm, sgn, da.recip, mirror);
       v[r] = make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
     }
   }
@@ -562,7 +590,8 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
 #pragma unroll
   for (int b = 0; b < 16 / RL; ++b)
 #pragma unroll
-    for (int r = 0; r < RL; ++r) col[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
+    for (int r = 0; r < RL; ++r)
+      col[col_off(out_pos<M, SL>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -655,43 +684,60 @@ static int persistent_grid(int ncu, int per_cu, int items) {
   return nb < items ? nb : items;
 }
 
-template <int N>
-void launch_fused_n(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  constexpr int L = N / 2;
+template <int L>
+void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
   using C = RowCfg<L>;
-  const int M = N;
-  // LDS: rows kernels XR*(L+L/16)*16 B, cols (M+M/16)*16 B -> blocks per CU (160 KB)
-  constexpr int row_lds = C::XR * Plan<L>::ROWSTRIDE * 16 + sizeof(TwLds<L>) + sizeof(TwLds<N>);
-  constexpr int col_lds = Plan<N>::PAD * 16;
-  const int row_per_cu = (160 * 1024) / row_lds;
-  const int col_per_cu = (160 * 1024) / col_lds;
-  if (pass == 0) {
-    hipLaunchKernelGGL(rows_fwd_kernel<L>, dim3(persistent_grid(a.ncu, row_per_cu, M / C::XR)),
-                       dim3(C::THREADS), 0, st, a.f, a.H, M, a.twL, a.twN);
-  } else if (pass == 1) {
-    DivArgs da{a.cx, a.cy, a.aa, a.bb, a.cc, a.scale, L, a.neg ? 1 : 0, a.recip ? 1 : 0};
-    (void)col_per_cu;
-    hipLaunchKernelGGL(cols_kernel<N>, dim3(L), dim3(Plan<N>::T), 0, st, a.H, a.twN, da);
-  } else {
-    hipLaunchKernelGGL(rows_inv_kernel<L>, dim3(persistent_grid(a.ncu, row_per_cu, M / C::XR)),
-                       dim3(C::THREADS), 0, st, a.H, a.s, M, a.twL, a.twN);
-  }
-  CFDJ_HIP(hipGetLastError());
+  constexpr int row_lds = C::XR * Plan<L>::ROWSTRIDE * 16 + sizeof(TwLds<L>) +
+                          sizeof(TwLds<2 * L>);
+  const int per_cu = (160 * 1024) / row_lds;
+  const dim3 grid(persistent_grid(a.ncu, per_cu, a.rows / C::XR));
+  if (pass == 0)
+    hipLaunchKernelGGL(rows_fwd_kernel<L>, grid, dim3(C::THREADS), 0, st, a.f, a.H, a.rows,
+                       a.twL, a.twN);
+  else
+    hipLaunchKernelGGL(rows_inv_kernel<L>, grid, dim3(C::THREADS), 0, st, a.H, a.s, a.rows,
+                       a.twL, a.twN);
 }
+
+template <int M>
+void launch_cols(const FusedPoissonArgs& a, hipStream_t st) {
+  DivArgs da{a.cx,  a.cy,  a.cy_mirror,        a.aa, a.bb, a.cc,       a.scale,
+             a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg};
+  hipLaunchKernelGGL(cols_kernel<M>, dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, a.twM, da);
+}
+
+constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 }  // namespace
 
-bool fused_poisson_supported(int nx, int ny) {
-  return nx == ny && (nx == 1024 || nx == 2048 || nx == 4096);
+// Row lengths nx = 1024..16384 (half-length L = 512..8192 in one workgroup's LDS), column
+// lengths ny = 1024..8192, powers of two; `rows` (this GPU's rows) a multiple of the row
+// pass's rows per work item (<= 8).
+bool fused_poisson_supported(int nx, int ny, int rows) {
+  return pow2(nx) && pow2(ny) && nx >= 1024 && nx <= 16384 && ny >= 1024 && ny <= 8192 &&
+         rows >= 8 && rows % 8 == 0 && ny % rows == 0;
 }
 
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  switch (a.n) {
-    case 1024: launch_fused_n<1024>(pass, a, st); break;
-    case 2048: launch_fused_n<2048>(pass, a, st); break;
-    case 4096: launch_fused_n<4096>(pass, a, st); break;
-    default: throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
+  if (!fused_poisson_supported(a.nx, a.ny, a.rows) || a.kb < 1 || (1 << a.rl_log2) > a.ny)
+    throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
+  if (pass == 1) {
+    switch (a.ny) {
+      case 1024: launch_cols<1024>(a, st); break;
+      case 2048: launch_cols<2048>(a, st); break;
+      case 4096: launch_cols<4096>(a, st); break;
+      case 8192: launch_cols<8192>(a, st); break;
+    }
+  } else {
+    switch (a.nx) {
+      case 1024: launch_rows<512>(pass, a, st); break;
+      case 2048: launch_rows<1024>(pass, a, st); break;
+      case 4096: launch_rows<2048>(pass, a, st); break;
+      case 8192: launch_rows<4096>(pass, a, st); break;
+      case 16384: launch_rows<8192>(pass, a, st); break;
+    }
   }
+  CFDJ_HIP(hipGetLastError());
 }
 
 }  // namespace cfdj

@@ -45,6 +45,10 @@ class PoissonFFT:
         """path: "auto" | "rocfft" | "fused" (CFDJ_POISSON_*)."""
         check(_lib.load().cfdj_fps_set_poisson(self._h, _PATHS[path]), "cfdj_fps_set_poisson")
 
+    def poisson(self):
+        return {_lib.POISSON_FUSED: "fused", _lib.POISSON_ROCFFT: "rocfft"}[
+            _lib.load().cfdj_fps_get_poisson(self._h)]
+
     def solve_device(self, f_ptr, s_ptr):
         check(_lib.load().cfdj_fps_solve_device(self._h, C.c_void_p(f_ptr), C.c_void_p(s_ptr)),
               "cfdj_fps_solve_device")

@@ -46,7 +46,8 @@ extern "C" {
 /* Poisson implementation (cfdj_vm_set_poisson / cfdj_fps_set_poisson). */
 #define CFDJ_POISSON_AUTO 0   /* fused where supported, rocFFT otherwise (default) */
 #define CFDJ_POISSON_ROCFFT 1 /* rocFFT D2Z + divide kernel + rocFFT Z2D */
-#define CFDJ_POISSON_FUSED 2  /* hand-written 3-pass FFT (square 1024/2048/4096 grids) */
+#define CFDJ_POISSON_FUSED 2  /* hand-written 3-pass FFT: power-of-two nx 1024..16384,
+                                 ny 1024..8192, power-of-two rank counts */
 
 /* Poisson symbol (cfdj_fps_set_symbol). */
 #define CFDJ_SYMBOL_FD 0       /* Common.jl:119-121 / fft_p.jl:37-39: aa + bb cos kx + cc cos ky */
@@ -76,6 +77,8 @@ int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long 
 int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
 /* Select the Poisson implementation (CFDJ_POISSON_*); ARG error if unsupported. */
 int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path);
+/* The implementation in use (CFDJ_POISSON_ROCFFT or CFDJ_POISSON_FUSED; ARG on NULL). */
+int cfdj_fps_get_poisson(cfdj_fps_plan* h);
 /* Select the symbol: CFDJ_SYMBOL_FD (default, fps/ps_fft) or CFDJ_SYMBOL_SPECTRAL
  * (fft_s.jl:8-37 ps_spectral: kx = 2pi/(nx dx) * index, kx[1] = eps, ky = kx). */
 int cfdj_fps_set_symbol(cfdj_fps_plan* h, int kind);
@@ -136,7 +139,7 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
 /* Replay cfdj_vm_step's kernel sequence from a captured HIP graph (default on; used on
  * single-GPU handles with the fused Poisson path, others launch eagerly). */
 int cfdj_vm_set_graph(cfdj_vm* h, int enable);
-/* Select / query the Poisson implementation (CFDJ_POISSON_*; single-GPU handles). */
+/* Select / query the Poisson implementation (CFDJ_POISSON_*; single-GPU and slab handles). */
 int cfdj_vm_set_poisson(cfdj_vm* h, int path);
 int cfdj_vm_get_poisson(cfdj_vm* h);
 void cfdj_vm_destroy(cfdj_vm* h);

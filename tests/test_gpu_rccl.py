@@ -12,22 +12,26 @@ from oracle import vm_oracle as vo
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("n,steps", [(64, 5), (256, 5)])
-def test_gpu_rccl_one_rank_slab(monkeypatch, n, steps):
+@pytest.mark.parametrize("n,steps,path", [(64, 5, "rocfft"), (256, 5, "rocfft"),
+                                          (1024, 3, "fused"), (1024, 3, "rocfft")])
+def test_gpu_rccl_one_rank_slab(monkeypatch, n, steps, path):
     from cfd_julia_amd import VortexMerger, _lib
 
     _lib.require_gpu()
     monkeypatch.setenv("CFDJ_FORCE_SLAB", "1")
     dx, dy, x, y = vo.vm_grid(n, n)
     w0 = vo.vm_ic(n, n, x, y)
-    ref = vo.numerical(w0, steps, 0.01, dx, dy, 1000.0)
+    dt = min(0.01, 5e-4 * (4096 / n) ** 2)
+    ref = vo.numerical(w0, steps, dt, dx, dy, 1000.0)
     uid = VortexMerger.unique_id()
     with VortexMerger(n, n, dx, dy, 1000.0, device=0, kind="dist", nranks=1, rank=0,
                       nccl_id=uid) as h:
         assert h.slab() == (0, n)
+        h.set_poisson(path)
+        assert h.poisson() == path
         h.upload_interior(w0)
         h.set_timing(True)
-        h.step(0.01, steps)
+        h.step(dt, steps)
         t = h.timing()
         w = h.download_interior()
     assert t["comm"][1] > 0  # the RCCL transposes / halos ran
