@@ -8,8 +8,14 @@
 One "step" = one full RK3 step (3 RHS evaluations = 3 FFT Poisson solves + 3 fused
 Arakawa/Laplacian/RK stage kernels) over the whole grid, all data resident in HBM.
 N = 1 runs BASELINE.json config 3 (4096^2, re = 1000, dt = 5e-4: the reference's dt = .01
-is unstable at this size).  N > 1 is weak scaling on the y-slab ladder
-4096^2 -> 5760^2 -> 8192^2 -> 11520^2 (~16.7 M cells per GPU), RCCL halos + all-to-all.
+is unstable at this size).  N > 1 is weak scaling on y-slabs with exactly
+4096^2 cells per GPU: 8192x4096 (N=2), 8192^2 (N=4, BASELINE config 5), 16384x8192 (N=8)
+-- power-of-two sides so every rank runs the hand-written FFT passes, ny <= nx as the
+reference's ky = kx table requires (Common.jl:113).  RCCL halos + all-to-all.
+
+Rehearsals on one GPU (not the headline): --virtual P runs the y-slab code with P virtual
+ranks (device copies for the transposes); --dist runs the RCCL slab code with a one-rank
+communicator (CFDJ_FORCE_SLAB=1).
 
 Rank 0 prints ONE JSON line (metric / value = whole-job MLUPS, roofline of the fused stage
 kernel from live HIP-event timing, cpu_baseline = the NumPy oracle on this host).
@@ -30,21 +36,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Poisson 32 per solve (D2Z read 8 + write ~8, Z2D read ~8 + write 8; divide fused).
 STAGE_BYTES_PER_CELL_STEP = 24 + 32 + 32
 STEP_BYTES_PER_CELL = 184
-WEAK_LADDER = {1: 4096, 2: 5760, 4: 8192, 8: 11520}
+WEAK_LADDER = {1: (4096, 4096), 2: (8192, 4096), 4: (8192, 8192), 8: (16384, 8192),
+               16: (16384, 16384)}
 
 
-def grid_for(n_gpus, nx_override=None):
-    if nx_override:
-        return nx_override
+def grid_for(n_gpus, nx=None, ny=None):
+    if nx:
+        return nx, ny or nx
     if n_gpus in WEAK_LADDER:
         return WEAK_LADDER[n_gpus]
     step = 128 * n_gpus // math.gcd(128, n_gpus)
-    return max(step, int(round(4096 * math.sqrt(n_gpus) / step)) * step)
+    n = max(step, int(round(4096 * math.sqrt(n_gpus) / step)) * step)
+    return n, n
 
 
-def stable_dt(nx):
-    # 5e-4 at 4096^2 (RK3 viscous limit 7.39e-4), scaled with dx^2
-    return 5e-4 * (4096.0 / nx) ** 2
+def stable_dt(nx, ny=None):
+    # 5e-4 at 4096^2 (RK3 viscous limit 7.39e-4), scaled with 1/(1/dx^2 + 1/dy^2)
+    ny = ny or nx
+    return 5e-4 * 2.0 * 4096.0 ** 2 / (nx ** 2 + ny ** 2)
 
 
 def load_pmc(nx):
@@ -61,20 +70,20 @@ def load_pmc(nx):
     return d
 
 
-def cpu_baseline(nx, steps, workers):
+def cpu_baseline(nx, ny, steps, workers):
     """The CPU oracle (NumPy + scipy.fft restatement of vm.jl/Common.jl) on this host."""
     from oracle import vm_oracle as vo
 
-    dx, dy, x, y = vo.vm_grid(nx, nx)
-    w = vo.vm_ic(nx, nx, x, y)
-    dt = stable_dt(nx)
+    dx, dy, x, y = vo.vm_grid(nx, ny)
+    w = vo.vm_ic(nx, ny, x, y)
+    dt = stable_dt(nx, ny)
     t0 = time.perf_counter()
     for _ in range(steps):
         w = vo.rk3_step(w, dt, dx, dy, 1000.0, workers=workers)
     t = time.perf_counter() - t0
-    return {"value": round(nx * nx * steps / t / 1e6, 4), "unit": "MLUPS", "cores": workers,
+    return {"value": round(nx * ny * steps / t / 1e6, 4), "unit": "MLUPS", "cores": workers,
             "kind": "port",
-            "sample": f"{steps} RK3 steps of the {nx}^2 vortex merger, NumPy oracle "
+            "sample": f"{steps} RK3 steps of the {nx}x{ny} vortex merger, NumPy oracle "
                       f"(oracle/vm_oracle.py; scipy.fft workers={workers}, stencil single-"
                       f"threaded NumPy), {t:.1f} s; Julia reference not runnable here"}
 
@@ -85,6 +94,12 @@ def main():
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nx", type=int, default=None, help="override the grid size")
+    ap.add_argument("--ny", type=int, default=None)
+    ap.add_argument("--virtual", type=int, default=0,
+                    help="one-GPU rehearsal: y-slab code with this many virtual ranks")
+    ap.add_argument("--dist", action="store_true",
+                    help="one-GPU rehearsal: RCCL slab code with a one-rank communicator")
+    ap.add_argument("--poisson", default="auto", choices=["auto", "fused", "rocfft", "schur"])
     ap.add_argument("--rows-per-wave", type=int, default=None)
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -117,30 +132,36 @@ def main():
         if world > 1:
             dist.barrier()
 
-    nx = ny = grid_for(n_gpus, args.nx)
-    dx = dy = 2 * math.pi / nx
-    dt = stable_dt(nx)
+    nx, ny = grid_for(n_gpus, args.nx, args.ny)
+    dx, dy = 2 * math.pi / nx, 2 * math.pi / ny
+    dt = stable_dt(nx, ny)
     re = 1000.0
 
-    if world > 1:
+    if args.dist:
+        os.environ["CFDJ_FORCE_SLAB"] = "1"
+    if world > 1 or args.dist:
         uid = VortexMerger.unique_id() if rank == 0 else bytes(128)
         t = torch.frombuffer(bytearray(uid), dtype=torch.uint8)
-        dist.broadcast(t, src=0)
+        if world > 1:
+            dist.broadcast(t, src=0)
         h = VortexMerger(nx, ny, dx, dy, re, device=local_rank, kind="dist", nranks=world,
                          rank=rank, nccl_id=bytes(t.numpy().tobytes()))
+    elif args.virtual:
+        h = VortexMerger(nx, ny, dx, dy, re, device=local_rank, kind="virtual",
+                         nranks=args.virtual)
     else:
         h = VortexMerger(nx, ny, dx, dy, re, device=local_rank)
+    h.set_poisson(args.poisson)
     if args.rows_per_wave:
         h.set_rows_per_wave(args.rows_per_wave)
 
-    # vm.jl:107-128 IC on the global grid (every rank uploads its own slab of it)
+    # vm.jl:107-128 IC on the global ghosted grid; each rank evaluates (and uploads) only
+    # its own rows -- np.zeros pages stay untouched elsewhere, so host memory is one slab
     x = dx * np.arange(nx + 1)
-    wn = np.empty((nx + 2, ny + 2), order="F")
-    vm_ic(nx, ny, x, x, wn)
-    wn[0, :] = wn[nx, :]
-    wn[:, 0] = wn[:, ny]
-    wn[nx + 1, :] = wn[1, :]
-    wn[:, ny + 1] = wn[:, 1]
+    y = dy * np.arange(ny + 1)
+    row0, rows = h.slab()
+    wn = np.zeros((nx + 2, ny + 2), order="F")
+    vm_ic(nx, rows - 1, x, y[row0:], wn[:, row0:])  # fills wn[1:nx+2, row0+1:row0+rows+1]
     h.upload(wn)
     del wn
 
@@ -180,6 +201,11 @@ def main():
     h.set_check_finite(True)
     h.sync()
 
+    parallelism = "single" if n_gpus == 1 else f"yslab{n_gpus}"
+    if args.virtual:
+        parallelism = f"virtual-yslab{args.virtual} (1 GPU rehearsal)"
+    elif args.dist and world == 1:
+        parallelism = "rccl-yslab1 (1 GPU rehearsal)"
     cells = nx * ny
     value = cells * args.steps / elapsed / 1e6
     ms_step = elapsed * 1e3 / max(args.steps, 1)
@@ -224,17 +250,17 @@ def main():
         "data": "synthetic: vm_ic two-Gaussian vortex-merger IC (Common.jl:208-219)",
         "config": {"workload": f"NS2D vortex merger {nx}x{ny} periodic, Arakawa + FD-FFT "
                                f"Poisson + SSP-RK3 (vm.jl)", "nx": nx, "ny": ny, "dt": dt,
-                   "re": re, "parallelism": "single" if n_gpus == 1 else f"yslab{n_gpus}"},
+                   "re": re, "parallelism": parallelism, "poisson": h.poisson()},
         "ms_per_step_instrumented": round(elapsed_i * 1e3 / args.steps, 4) if elapsed_i else None,
         "achieved_hbm_gbs_step": round(step_gbs, 1),
         "step_roofline_frac": round(step_gbs / HBM_PEAK_GBS, 4),
         "kernels": breakdown,
         "roofline": roofline,
     }
-    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline:
+    if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.virtual:
         workers = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
                       or os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(nx, args.cpu_steps, workers)
+        line["cpu_baseline"] = cpu_baseline(nx, ny, args.cpu_steps, workers)
     if rank == 0:
         print(json.dumps(line), flush=True)
     h.close()

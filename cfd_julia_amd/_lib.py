@@ -21,7 +21,7 @@ ERR_NAMES = {-1: "CFDJ_ERR_ARG", -2: "CFDJ_ERR_HIP", -3: "CFDJ_ERR_ROCFFT",
              -4: "CFDJ_ERR_RCCL", -5: "CFDJ_ERR_NONFINITE", -6: "CFDJ_ERR_STATE"}
 K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
-POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED = 0, 1, 2
+POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED, POISSON_SCHUR = 0, 1, 2, 3
 SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1
 CAVITY_DST, CAVITY_MG = 0, 1
 

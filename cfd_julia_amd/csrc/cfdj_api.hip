@@ -95,6 +95,12 @@ struct cfdj_vm {
   double2* spec = nullptr;                                       // Single
   Fused fused;                                                   // Single, 2^k grids
   bool use_fused = false;
+  // substructured y-slab solve (schur.hip): traces of all ranks T, gathered column G
+  SchurTables schur;
+  bool use_schur = false;
+  double2* T = nullptr;
+  double2* G = nullptr;
+  rocfft_plan g_fwd = nullptr, g_inv = nullptr;
   ncclComm_t comm = nullptr;
   double* gather = nullptr;                                      // Rccl download buffer
   // timing
@@ -205,6 +211,10 @@ struct cfdj_vm {
 
   // ---- Poisson: psi = fps(-w)  (Common.jl:134-136) ------------------------------------
   void poisson(const std::vector<const double*>& src, bool neg) {
+    if (use_schur) {
+      poisson_schur(src, neg);
+      return;
+    }
     if (!slab_mode() && use_fused) {
       const FusedPoissonArgs a = fused.args(sym, src[0], slabs[0].psi, spec, neg);
       static const int cat[3] = {CFDJ_K_FFT_FWD, CFDJ_K_DIVIDE, CFDJ_K_FFT_INV};
@@ -286,6 +296,72 @@ struct cfdj_vm {
       tend();
       tbegin(CFDJ_K_FFT_INV);
       plans.exec(row_inv, s.X, s.psi);
+      tend();
+    }
+  }
+
+  // y-slabs without a transpose (schur.hip): row r2c -> interior traces -> all-gather of
+  // 4 numbers per x-mode -> separator solve + interior solve -> row c2r.  The packed
+  // DC / Nyquist column is gathered and solved with the reference symbol by rocFFT.
+  void poisson_schur(const std::vector<const double*>& src, bool neg) {
+    const int L = nx / 2;
+    const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
+    const size_t colb = (size_t)rows * sizeof(double2);
+    std::vector<FusedPoissonArgs> a;
+    for (size_t i = 0; i < slabs.size(); ++i)
+      a.push_back(fused.args(sym, src[i], slabs[i].psi, slabs[i].X, slabs[i].X, rows,
+                             slabs[i].rank, nranks, neg));
+    for (auto& ai : a) {
+      tbegin(CFDJ_K_FFT_FWD);
+      launch_fused_poisson_pass(0, ai, stream);
+      tend();
+    }
+    tbegin(CFDJ_K_COMM);
+    for (auto& s : slabs)
+      CFDJ_HIP(hipMemcpyAsync(G + s.row0, s.X, colb, hipMemcpyDeviceToDevice, stream));
+    if (mode == Mode::Rccl)
+      CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, stream));
+    tend();
+    for (auto& s : slabs) {
+      tbegin(CFDJ_K_DIVIDE);
+      launch_schur_pass(0, schur.args(s.X, T, s.rank, out_scale, ny), stream);
+      tend();
+    }
+    if (mode == Mode::Rccl) {
+      tbegin(CFDJ_K_COMM);
+      const size_t cnt = (size_t)L * 4 * 2;  // doubles per rank
+      CFDJ_NCCL(ncclAllGather(reinterpret_cast<double*>(T) + (size_t)rank * cnt, T, cnt,
+                              ncclDouble, comm, stream));
+      tend();
+    }
+    tbegin(CFDJ_K_DIVIDE);
+    plans.exec(g_fwd, G, nullptr);
+    PackedDivParams pd;
+    pd.Z = G;
+    pd.cx = sym.cx;
+    pd.cy = sym.cy;
+    pd.aa = sym.aa;
+    pd.bb = sym.bb;
+    pd.cc = sym.cc;
+    pd.scale = sym.scale;
+    pd.L = L;
+    pd.ny = ny;
+    pd.neg = neg;
+    launch_packed_divide(pd, stream);
+    plans.exec(g_inv, G, nullptr);
+    tend();
+    for (auto& s : slabs) {
+      tbegin(CFDJ_K_DIVIDE);
+      launch_schur_pass(1, schur.args(s.X, T, s.rank, out_scale, ny), stream);
+      tend();
+    }
+    tbegin(CFDJ_K_COMM);
+    for (auto& s : slabs)
+      CFDJ_HIP(hipMemcpyAsync(s.X, G + s.row0, colb, hipMemcpyDeviceToDevice, stream));
+    tend();
+    for (auto& ai : a) {
+      tbegin(CFDJ_K_FFT_INV);
+      launch_fused_poisson_pass(2, ai, stream);
       tend();
     }
   }
@@ -439,6 +515,16 @@ struct cfdj_vm {
       col_inv = plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 1,
                           &len_y, kb, desc);
       rocfft_plan_description_destroy(desc);
+      if (schur_ok(nx, ny, nranks)) {
+        schur.init(nx, ny, dx, dy, eps, nranks);
+        T = dalloc<double2>((size_t)nranks * (nx / 2) * 4);
+        G = dalloc<double2>((size_t)ny);
+        g_fwd = plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 1,
+                          &len_y, 1, nullptr);
+        g_inv = plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 1,
+                          &len_y, 1, nullptr);
+        use_schur = true;
+      }
     } else {
       size_t lens[2] = {(size_t)nx, (size_t)ny};
       fwd2d = plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace, 2,
@@ -453,6 +539,7 @@ struct cfdj_vm {
       fused.init(nx, ny);
       use_fused = true;
     }
+    if (use_schur && !fused.ready()) fused.init(nx, ny);  // row-pass twiddles
   }
 
   ~cfdj_vm() {
@@ -462,6 +549,9 @@ struct cfdj_vm {
     plans.destroy();
     sym.destroy();
     fused.destroy();
+    schur.destroy();
+    dfree(T);
+    dfree(G);
     dfree(spec);
     dfree(gather);
     dfree(d_flag);
@@ -749,23 +839,36 @@ int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, doub
                 long lds) {
   return guard([&] {
     CFDJ_REQUIRE(h && w && r && s, "NULL argument");
-    CFDJ_REQUIRE(h->mode == Mode::Single, "cfdj_vm_rhs needs a single-GPU handle");
+    CFDJ_REQUIRE(h->mode != Mode::Rccl, "cfdj_vm_rhs needs a single-GPU or virtual-slab handle");
     check_ld(ldw, (long)h->nx + 2, "ldw");
     check_ld(ldr, (long)h->nx + 2, "ldr");
     check_ld(lds, (long)h->nx + 2, "lds");
     select_device(h->device);
     const int nx = h->nx, ny = h->ny;
-    Slab& sl = h->slabs[0];
-    CFDJ_HIP(hipMemcpy2DAsync(sl.wa, nx * sizeof(double), w + 1 + ldw, ldw * sizeof(double),
-                              nx * sizeof(double), ny, hipMemcpyHostToDevice, h->stream));
-    h->poisson({sl.wa}, true);
-    h->tbegin(CFDJ_K_STAGE);
-    launch_stage(0, h->stage_params(sl, sl.wa, sl.wa, sl.wb, 0.0), h->stream);
-    h->tend();
-    CFDJ_HIP(hipMemcpy2DAsync(r + 1 + ldr, ldr * sizeof(double), sl.wb, nx * sizeof(double),
-                              nx * sizeof(double), ny, hipMemcpyDeviceToHost, h->stream));
-    CFDJ_HIP(hipMemcpy2DAsync(s + 1 + lds, lds * sizeof(double), sl.psi, nx * sizeof(double),
-                              nx * sizeof(double), ny, hipMemcpyDeviceToHost, h->stream));
+    const size_t rowb = nx * sizeof(double);
+    std::vector<const double*> src;
+    for (auto& sl : h->slabs) {
+      CFDJ_HIP(hipMemcpy2DAsync(sl.wa, rowb, w + 1 + (size_t)(1 + sl.row0) * ldw,
+                                ldw * sizeof(double), rowb, sl.rows, hipMemcpyHostToDevice,
+                                h->stream));
+      src.push_back(sl.wa);
+    }
+    h->poisson(src, true);
+    if (h->slab_mode()) {
+      h->halo(false, src);
+      std::vector<const double*> ps;
+      for (auto& sl : h->slabs) ps.push_back(sl.psi);
+      h->halo(true, ps);
+    }
+    for (auto& sl : h->slabs) {
+      h->tbegin(CFDJ_K_STAGE);
+      launch_stage(0, h->stage_params(sl, sl.wa, sl.wa, sl.wb, 0.0), h->stream);
+      h->tend();
+      CFDJ_HIP(hipMemcpy2DAsync(r + 1 + (size_t)(1 + sl.row0) * ldr, ldr * sizeof(double), sl.wb,
+                                rowb, rowb, sl.rows, hipMemcpyDeviceToHost, h->stream));
+      CFDJ_HIP(hipMemcpy2DAsync(s + 1 + (size_t)(1 + sl.row0) * lds, lds * sizeof(double),
+                                sl.psi, rowb, rowb, sl.rows, hipMemcpyDeviceToHost, h->stream));
+    }
     CFDJ_HIP(hipStreamSynchronize(h->stream));
     h->harvest();
     ghost_fill(s, lds, nx, ny);
@@ -831,11 +934,18 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
 int cfdj_vm_set_poisson(cfdj_vm* h, int path) {
   return guard([&] {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
-    CFDJ_REQUIRE(path >= CFDJ_POISSON_AUTO && path <= CFDJ_POISSON_FUSED, "bad path");
+    CFDJ_REQUIRE(path >= CFDJ_POISSON_AUTO && path <= CFDJ_POISSON_SCHUR, "bad path");
     select_device(h->device);
-    const bool f = resolve_fused(path, h->nx, h->ny, h->nranks);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    const bool can_schur = h->slab_mode() && h->schur.ready();
+    if (path == CFDJ_POISSON_SCHUR && !can_schur)
+      throw Error{CFDJ_ERR_ARG, "substructured Poisson needs y-slabs of a square power-of-two "
+                                "grid with 512..4096 rows per rank"};
+    const bool sc = path == CFDJ_POISSON_SCHUR || (path == CFDJ_POISSON_AUTO && can_schur);
+    const bool f = sc ? h->use_fused : resolve_fused(path, h->nx, h->ny, h->nranks);
     if (f && !h->fused.ready()) h->fused.init(h->nx, h->ny);
     h->use_fused = f;
+    h->use_schur = sc;
     h->invalidate_graph();
   });
 }
@@ -852,6 +962,7 @@ int cfdj_vm_set_graph(cfdj_vm* h, int enable) {
 
 int cfdj_vm_get_poisson(cfdj_vm* h) {
   if (!h) return CFDJ_ERR_ARG;
+  if (h->use_schur) return CFDJ_POISSON_SCHUR;
   return h->use_fused ? CFDJ_POISSON_FUSED : CFDJ_POISSON_ROCFFT;
 }
 

@@ -144,7 +144,39 @@ struct FusedPoissonArgs {
   int ncu;              // compute units (persistent grid size)
 };
 bool fused_poisson_supported(int nx, int ny, int rows);
+bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);
+
+// Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
+// m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row
+// per rank (row 0 of each slab); interior blocks by DST-I (odd-extension FFT of length
+// 2 rl in LDS), separators by a P x P circulant system from the gathered traces.
+struct SchurArgs {
+  double2* H;           // this rank's column-major half spectrum, pitch rl (in place)
+  double2* T;           // [P][L][4] traces of every rank: f_sep, t_1, t_n, column sum
+  const double* e;      // e_m = d_m + cc (exact sum, rounded once), m < L
+  const double* q;      // q_k = 1 - cos(pi k / rl), k <= rl
+  const double* cinv;   // [L][P] first row of the inverse circulant separator system
+  const double* corr;   // [L] 1/D_ref(m, 0) - 1/e_m (the reference's ky[1] = eps)
+  const double2* tw;    // exp(-2 pi i k / (2 rl)), k < 2 rl
+  double cc, inv_dy2, out_scale, inv_ny;
+  int rl, L, P, rank;
+};
+bool schur_supported(int rl);
+void launch_schur_pass(int pass, const SchurArgs& a, hipStream_t st);  // 0 traces, 1 solve
+
+// The packed DC / Nyquist column (x-modes 0 and nx/2 as Re / Im of one complex column of
+// length ny), already FFT'd along y: split with Z[-k], divide each half by the reference
+// symbol of its x-mode (e[1,1] = 0), re-pack; in place.
+struct PackedDivParams {
+  double2* Z;
+  const double* cx;     // cos(kx[m]), m <= L
+  const double* cy;     // cos(ky[k]), k < ny
+  double aa, bb, cc, scale;
+  int L, ny;
+  bool neg;
+};
+void launch_packed_divide(const PackedDivParams& p, hipStream_t st);
 
 // Finiteness check: sets *flag = 1 if any element is not finite.
 void launch_check_finite(const double* a, size_t n, int* flag, hipStream_t st);

@@ -292,6 +292,108 @@ struct Fused {
   }
 };
 
+// Tables of the substructured y-slab solve (schur.hip), built in long double.
+struct SchurTables {
+  int rl = 0, L = 0, P = 0;
+  double cc = 0, inv_dy2 = 0;
+  double *e = nullptr, *q = nullptr, *cinv = nullptr, *corr = nullptr;
+  double2* tw = nullptr;
+  bool ready() const { return e != nullptr; }
+  void init(int nx, int ny, double dx, double dy, double eps, int nranks) {
+    typedef long double ld;
+    const ld pi = 3.141592653589793238462643383279502884L;
+    P = nranks;
+    rl = ny / nranks;
+    L = nx / 2;
+    const double aa = -2.0 / (dx * dx) - 2.0 / (dy * dy);
+    const double bb = 2.0 / (dx * dx);
+    cc = 2.0 / (dy * dy);
+    inv_dy2 = 1.0 / (dy * dy);
+    const std::vector<double> kx = kx_table(nx, eps);
+    const double ce = std::cos(kx[0]);  // reference cos(ky[1]) = cos(eps)
+    std::vector<double> he(L), hq(rl + 1), hc((size_t)L * P, 0.0), hr(L, 0.0);
+    std::vector<ld> s2(rl), qk(rl + 1);
+    for (int k = 0; k <= rl; ++k) {
+      const ld sn = sinl(pi * (ld)k / (ld)(2 * rl));
+      qk[k] = 2.0L * sn * sn;  // 1 - cos(pi k / rl) without cancellation
+      hq[k] = (double)qk[k];
+    }
+    for (int k = 1; k < rl; ++k) {
+      const ld sn = sinl(pi * (ld)k / (ld)rl);
+      s2[k] = sn * sn;
+    }
+    const ld dy4 = ((ld)dy * (ld)dy) * ((ld)dy * (ld)dy);
+    for (int m = 0; m < L; ++m) {
+      const double dm = aa + bb * std::cos(kx[m]);  // Common.jl:120 order (no FMA)
+      const ld em = (ld)dm + (ld)cc;                // constant-mode eigenvalue, exact sum
+      he[m] = (double)em;
+      if (m == 0) continue;  // packed DC / Nyquist column: gathered-column FFT
+      ld a1 = 0.0L, an = 0.0L;
+      for (int k = 1; k < rl; ++k) {
+        const ld t = s2[k] / (em - (ld)cc * qk[k]);
+        a1 += t;
+        an += (k & 1) ? t : -t;
+      }
+      a1 *= 2.0L / (ld)rl;
+      an *= 2.0L / (ld)rl;
+      const ld diag = (ld)dm - 2.0L * a1 / dy4, off = -an / dy4;
+      std::vector<ld> mu(P);
+      for (int j = 0; j < P; ++j) mu[j] = diag + 2.0L * off * cosl(2.0L * pi * j / P);
+      for (int d = 0; d < P; ++d) {
+        ld c = 0.0L;
+        for (int j = 0; j < P; ++j) c += cosl(2.0L * pi * (ld)j * d / P) / mu[j];
+        hc[(size_t)m * P + d] = (double)(c / P);
+      }
+      const double dref = (aa + bb * std::cos(kx[m])) + cc * ce;  // reference D(m, 0)
+      hr[m] = (double)(1.0L / (ld)dref - 1.0L / em);
+    }
+    e = dalloc<double>(L);
+    q = dalloc<double>(rl + 1);
+    cinv = dalloc<double>((size_t)L * P);
+    corr = dalloc<double>(L);
+    CFDJ_HIP(hipMemcpy(e, he.data(), L * sizeof(double), hipMemcpyHostToDevice));
+    CFDJ_HIP(hipMemcpy(q, hq.data(), (rl + 1) * sizeof(double), hipMemcpyHostToDevice));
+    CFDJ_HIP(hipMemcpy(cinv, hc.data(), hc.size() * sizeof(double), hipMemcpyHostToDevice));
+    CFDJ_HIP(hipMemcpy(corr, hr.data(), L * sizeof(double), hipMemcpyHostToDevice));
+    tw = twiddle_table(2 * rl);
+  }
+  void destroy() {
+    dfree(e);
+    dfree(q);
+    dfree(cinv);
+    dfree(corr);
+    dfree(tw);
+    e = q = cinv = corr = nullptr;
+    tw = nullptr;
+  }
+  SchurArgs args(double2* H, double2* T, int rank, double out_scale, int ny) const {
+    SchurArgs a;
+    a.H = H;
+    a.T = T;
+    a.e = e;
+    a.q = q;
+    a.cinv = cinv;
+    a.corr = corr;
+    a.tw = tw;
+    a.cc = cc;
+    a.inv_dy2 = inv_dy2;
+    a.out_scale = out_scale;
+    a.inv_ny = 1.0 / (double)ny;
+    a.rl = rl;
+    a.L = L;
+    a.P = P;
+    a.rank = rank;
+    return a;
+  }
+};
+
+// The substructured path: square power-of-two grids (the reference's ky = kx table is the
+// periodic y-symbol only when ny == nx), power-of-two rank counts, slabs of 512..4096 rows.
+inline bool schur_ok(int nx, int ny, int nranks) {
+  if (nx != ny || nranks < 1 || (nranks & (nranks - 1)) != 0 || ny % nranks != 0) return false;
+  return schur_supported(ny / nranks) && fused_rows_supported(nx, ny / nranks);
+}
+
 // The fused path on `nranks` y-slabs: power-of-two slabs whose column blocks split evenly.
 inline bool fused_ok(int nx, int ny, int nranks) {
   if (nranks < 1 || (nranks & (nranks - 1)) != 0 || ny % nranks != 0) return false;

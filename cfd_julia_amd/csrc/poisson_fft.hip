@@ -22,336 +22,12 @@
 // Twiddles come from host-built tables (long-double accurate) read through L1/L2.  FMA
 // contraction is allowed here: the FFT is not bit-comparable to FFTW / pocketfft anyway
 // (tolerance 1e-12 relative on psi, tests/test_gpu_parity.py).
-#include "cfdj_internal.hpp"
-
 #pragma clang fp contract(fast)
+#include "fft_lds.hpp"
 
 namespace cfdj {
 
 namespace {
-
-constexpr int ilog2(int n) { return n <= 1 ? 0 : 1 + ilog2(n / 2); }
-
-// exp(-2 pi i k/16) = (kC16[k], -kS16[k])
-__device__ constexpr double kC16[16] = {
-    1.0, 0.9238795325112867, 0.7071067811865476, 0.3826834323650898,
-    0.0, -0.3826834323650898, -0.7071067811865476, -0.9238795325112867,
-    -1.0, -0.9238795325112867, -0.7071067811865476, -0.3826834323650898,
-    0.0, 0.3826834323650898, 0.7071067811865476, 0.9238795325112867};
-__device__ constexpr double kS16[16] = {
-    0.0, 0.3826834323650898, 0.7071067811865476, 0.9238795325112867,
-    1.0, 0.9238795325112867, 0.7071067811865476, 0.3826834323650898,
-    0.0, -0.3826834323650898, -0.7071067811865476, -0.9238795325112867,
-    -1.0, -0.9238795325112867, -0.7071067811865476, -0.3826834323650898};
-
-__device__ __forceinline__ double2 cadd(double2 a, double2 b) { return make_double2(a.x + b.x, a.y + b.y); }
-__device__ __forceinline__ double2 csub(double2 a, double2 b) { return make_double2(a.x - b.x, a.y - b.y); }
-__device__ __forceinline__ double2 cmul(double2 a, double2 b) {
-  return make_double2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
-}
-__device__ __forceinline__ double2 cconj(double2 a) { return make_double2(a.x, -a.y); }
-
-// v * W16^K (DIR = -1 forward, +1 inverse)
-template <int K, int DIR>
-__device__ __forceinline__ double2 tw16(double2 v) {
-  constexpr int k = K & 15;
-  if constexpr (k == 0) {
-    return v;
-  } else if constexpr (k == 4) {  // -i (fwd) / +i (inv)
-    return DIR < 0 ? make_double2(v.y, -v.x) : make_double2(-v.y, v.x);
-  } else if constexpr (k == 8) {
-    return make_double2(-v.x, -v.y);
-  } else if constexpr (k == 12) {
-    return DIR < 0 ? make_double2(-v.y, v.x) : make_double2(v.y, -v.x);
-  } else {
-    constexpr double c = kC16[k];
-    constexpr double s = DIR < 0 ? -kS16[k] : kS16[k];
-    return make_double2(v.x * c - v.y * s, v.x * s + v.y * c);
-  }
-}
-
-template <int DIR>
-__device__ __forceinline__ void dft2(double2& a, double2& b) {
-  const double2 t = a;
-  a = cadd(t, b);
-  b = csub(t, b);
-}
-
-template <int DIR>
-__device__ __forceinline__ void dft4(double2& x0, double2& x1, double2& x2, double2& x3) {
-  const double2 s02 = cadd(x0, x2), d02 = csub(x0, x2);
-  const double2 s13 = cadd(x1, x3), d13 = tw16<4, DIR>(csub(x1, x3));
-  x0 = cadd(s02, s13);
-  x2 = csub(s02, s13);
-  x1 = cadd(d02, d13);
-  x3 = csub(d02, d13);
-}
-
-// In-register DFT of length R on v[0..R-1] (natural order in, natural order out).
-template <int R, int DIR>
-__device__ __forceinline__ void dft(double2* v) {
-  if constexpr (R == 2) {
-    dft2<DIR>(v[0], v[1]);
-  } else if constexpr (R == 4) {
-    dft4<DIR>(v[0], v[1], v[2], v[3]);
-  } else if constexpr (R == 8) {
-    // n = 4 n1 + n2 (n1 < 2, n2 < 4), k = k1 + 2 k2
-    double2 a[4][2];
-#pragma unroll
-    for (int n2 = 0; n2 < 4; ++n2) {
-      a[n2][0] = v[n2];
-      a[n2][1] = v[4 + n2];
-      dft2<DIR>(a[n2][0], a[n2][1]);
-    }
-    a[1][1] = tw16<2, DIR>(a[1][1]);
-    a[2][1] = tw16<4, DIR>(a[2][1]);
-    a[3][1] = tw16<6, DIR>(a[3][1]);
-#pragma unroll
-    for (int k1 = 0; k1 < 2; ++k1) {
-      dft4<DIR>(a[0][k1], a[1][k1], a[2][k1], a[3][k1]);
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 2 * k2] = a[k2][k1];
-    }
-  } else {
-    static_assert(R == 16, "radix");
-    // n = 4 n1 + n2, k = k1 + 4 k2
-    double2 a[4][4];
-#pragma unroll
-    for (int n2 = 0; n2 < 4; ++n2) {
-      a[n2][0] = v[n2];
-      a[n2][1] = v[4 + n2];
-      a[n2][2] = v[8 + n2];
-      a[n2][3] = v[12 + n2];
-      dft4<DIR>(a[n2][0], a[n2][1], a[n2][2], a[n2][3]);
-    }
-    a[1][1] = tw16<1, DIR>(a[1][1]);
-    a[1][2] = tw16<2, DIR>(a[1][2]);
-    a[1][3] = tw16<3, DIR>(a[1][3]);
-    a[2][1] = tw16<2, DIR>(a[2][1]);
-    a[2][2] = tw16<4, DIR>(a[2][2]);
-    a[2][3] = tw16<6, DIR>(a[2][3]);
-    a[3][1] = tw16<3, DIR>(a[3][1]);
-    a[3][2] = tw16<6, DIR>(a[3][2]);
-    a[3][3] = tw16<9, DIR>(a[3][3]);
-#pragma unroll
-    for (int k1 = 0; k1 < 4; ++k1) {
-      dft4<DIR>(a[0][k1], a[1][k1], a[2][k1], a[3][k1]);
-#pragma unroll
-      for (int k2 = 0; k2 < 4; ++k2) v[k1 + 4 * k2] = a[k2][k1];
-    }
-  }
-}
-
-// Stockham plan of a length-L transform: radix-16 stages, then one remainder stage.
-template <int L>
-struct Plan {
-  static constexpr int LOG = ilog2(L);
-  static constexpr int N16 = LOG / 4;
-  static constexpr int REM = 1 << (LOG % 4);
-  static constexpr int NSTAGES = N16 + (REM > 1 ? 1 : 0);
-  static constexpr int T = L / 16;  // threads per transform
-  static constexpr int radix(int s) { return s < N16 ? 16 : REM; }
-  static constexpr int ns(int s) { return s == 0 ? 1 : ns(s - 1) * radix(s - 1); }
-  static constexpr int PAD = L + L / 16;  // LDS elements per transform (1 pad per 16)
-  static constexpr int ROWSTRIDE = PAD;  // rows kernels: row stride (= 0 mod 64 banks)
-};
-
-__device__ __forceinline__ int padx(int i) { return i + (i >> 4); }
-
-// The FD symbol aa + bb cos kx + cc cos ky, evaluated exactly as Common.jl:120 writes it
-// (no FMA): for kx = eps the sum cancels to O(1) from terms of O(nx^2), so a contracted
-// bb*cx changes psi by ~1e-11 relative at 4096^2 (measured) -- well outside parity.
-__device__ __forceinline__ double fd_symbol_x(double aa, double bb, double cx) {
-#pragma clang fp contract(off)
-  return aa + bb * cx;
-}
-__device__ __forceinline__ double fd_symbol(double ax, double cc, double cy) {
-#pragma clang fp contract(off)
-  return ax + cc * cy;
-}
-
-// Twiddles live in LDS as a 2-level table, W_L^e = hi[e >> 6] * lo[e & 63] (one rounding),
-// filled once per persistent workgroup from the host-built long-double tables.  Keeping
-// them out of the vector-memory stream matters: vmcnt is in order, so a twiddle load issued
-// behind the next item's HBM prefetch would wait for that whole prefetch.
-template <int L>
-struct TwLds {
-  static constexpr int HI = L / 64 > 0 ? L / 64 : 1;
-  double2 lo[64];
-  double2 hi[HI];
-  __device__ __forceinline__ void fill(const double2* __restrict__ tw) {
-    for (int i = threadIdx.x; i < 64 + HI; i += blockDim.x) {
-      if (i < 64) lo[i] = tw[i];
-      else hi[i - 64] = tw[(i - 64) * 64];
-    }
-  }
-  __device__ __forceinline__ double2 w(int e) const { return cmul(hi[e >> 6], lo[e & 63]); }
-};
-
-// The same interface over the global long-double table (L2-resident): used where no HBM
-// prefetch is queued ahead of the twiddle loads (the non-persistent column pass).
-template <int L>
-struct TwGlobal {
-  const double2* __restrict__ t;
-  __device__ __forceinline__ double2 w(int e) const { return t[e]; }
-};
-
-// Twiddles of one butterfly: w1 = W^e, w4 = W^{4e} (R >= 8) for the stage's base exponent
-// e = (j mod NS) * L/(NS*R).
-template <int L, int R, int NS>
-struct Tw {
-  double2 w1, w4;
-};
-template <int L, int R, int NS, class TW>
-__device__ __forceinline__ Tw<L, R, NS> load_tw(int j, const TW& tw) {
-  Tw<L, R, NS> t;
-  if constexpr (NS > 1) {
-    const int e = (j & (NS - 1)) * (L / (NS * R));
-    t.w1 = tw.w(e);
-    if constexpr (R >= 8) t.w4 = tw.w(4 * e);
-  }
-  return t;
-}
-
-// Twiddle the R inputs of butterfly j (Stockham stage with stride NS) and run the DFT.
-template <int L, int R, int NS, int DIR>
-__device__ __forceinline__ void butterfly(double2* v, const Tw<L, R, NS>& t) {
-  if constexpr (NS > 1) {
-    const double2 w1 = DIR < 0 ? t.w1 : cconj(t.w1);
-    if constexpr (R == 2) {
-      v[1] = cmul(v[1], w1);
-    } else {
-      const double2 w2 = cmul(w1, w1), w3 = cmul(w2, w1);
-      v[1] = cmul(v[1], w1);
-      v[2] = cmul(v[2], w2);
-      v[3] = cmul(v[3], w3);
-      if constexpr (R >= 8) {
-        const double2 w4 = DIR < 0 ? t.w4 : cconj(t.w4);
-        v[4] = cmul(v[4], w4);
-        v[5] = cmul(v[5], cmul(w4, w1));
-        v[6] = cmul(v[6], cmul(w4, w2));
-        v[7] = cmul(v[7], cmul(w4, w3));
-        if constexpr (R == 16) {
-          const double2 w8 = cmul(w4, w4), w12 = cmul(w8, w4);
-          v[8] = cmul(v[8], w8);
-          v[9] = cmul(v[9], cmul(w8, w1));
-          v[10] = cmul(v[10], cmul(w8, w2));
-          v[11] = cmul(v[11], cmul(w8, w3));
-          v[12] = cmul(v[12], w12);
-          v[13] = cmul(v[13], cmul(w12, w1));
-          v[14] = cmul(v[14], cmul(w12, w2));
-          v[15] = cmul(v[15], cmul(w12, w3));
-        }
-      }
-    }
-  }
-  dft<R, DIR>(v);
-}
-
-// Stage S of the plan on the thread's 16 registers (16/R butterflies of radix R):
-// inputs v[b*R + r] = element (j_b + r*L/R), j_b = tid + b*T.
-template <int L, int S>
-struct StageTw {
-  static constexpr int R = Plan<L>::radix(S);
-  static constexpr int NS = Plan<L>::ns(S);
-  Tw<L, R, NS> t[16 / R];
-};
-template <int L, int S, class TW>
-__device__ __forceinline__ StageTw<L, S> stage_tw(int tid, const TW& tw) {
-  StageTw<L, S> st;
-#pragma unroll
-  for (int b = 0; b < 16 / StageTw<L, S>::R; ++b)
-    st.t[b] = load_tw<L, StageTw<L, S>::R, StageTw<L, S>::NS, TW>(tid + b * Plan<L>::T, tw);
-  return st;
-}
-template <int L, int S, int DIR>
-__device__ __forceinline__ void stage_regs(double2 (&v)[16], const StageTw<L, S>& st) {
-  constexpr int R = Plan<L>::radix(S);
-  constexpr int NS = Plan<L>::ns(S);
-#pragma unroll
-  for (int b = 0; b < 16 / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);
-}
-template <int L, int S, int DIR, class TW>
-__device__ __forceinline__ void stage_regs(double2 (&v)[16], int tid, const TW& tw) {
-  stage_regs<L, S, DIR>(v, stage_tw<L, S, TW>(tid, tw));
-}
-
-// Stage input / output positions.
-template <int L, int S>
-__device__ __forceinline__ int in_pos(int tid, int b, int r) {
-  using P = Plan<L>;
-  constexpr int R = P::radix(S);
-  return tid + b * P::T + r * (L / R);
-}
-template <int L, int S>
-__device__ __forceinline__ int out_pos(int tid, int b, int r) {
-  using P = Plan<L>;
-  constexpr int R = P::radix(S);
-  constexpr int NS = P::ns(S);
-  const int j = tid + b * P::T;
-  return (j / NS) * NS * R + (j & (NS - 1)) + r * NS;
-}
-
-// LDS element p of a transform lives at buf[IL * padx(p)]: IL = 1 for one transform per
-// buffer (rows), IL = 2 for the two interleaved columns of a tile (cols), so consecutive
-// lanes -- (tid, c) pairs -- touch consecutive 16-B slots.
-template <int L, int S, int IL = 1>
-__device__ __forceinline__ void lds_write(double2* buf, const double2 (&v)[16], int tid) {
-  constexpr int R = Plan<L>::radix(S);
-#pragma unroll
-  for (int b = 0; b < 16 / R; ++b)
-#pragma unroll
-    for (int r = 0; r < R; ++r) buf[IL * padx(out_pos<L, S>(tid, b, r))] = v[b * R + r];
-}
-template <int L, int S, int IL = 1>
-__device__ __forceinline__ void lds_read(const double2* buf, double2 (&v)[16], int tid) {
-  constexpr int R = Plan<L>::radix(S);
-#pragma unroll
-  for (int b = 0; b < 16 / R; ++b)
-#pragma unroll
-    for (int r = 0; r < R; ++r) v[b * R + r] = buf[IL * padx(in_pos<L, S>(tid, b, r))];
-}
-
-// Middle stages S0..NSTAGES-1 (each: read LDS, barrier, compute, write LDS, barrier).
-// The caller has written stage S0-1's output to LDS and synchronised.
-template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW>
-__device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[16], int tid,
-                                           const TW& tw) {
-  using P = Plan<L>;
-  if constexpr (S < P::NSTAGES) {
-    const StageTw<L, S> st = stage_tw<L, S, TW>(tid, tw);
-    lds_read<L, S, IL>(buf, v, tid);
-    __syncthreads();
-    stage_regs<L, S, DIR>(v, st);
-    if constexpr (S + 1 < P::NSTAGES || LAST_TO_LDS) {
-      lds_write<L, S, IL>(buf, v, tid);
-      __syncthreads();
-    }
-    run_stages<L, S + 1, DIR, LAST_TO_LDS, IL, TW>(buf, v, tid, tw);
-  }
-}
-
-// Persistent work split: `nb` resident workgroups (a multiple of 8) process items [0, n).
-// XCD x = b % 8 owns the contiguous item range [x n/8, (x+1) n/8); its S = nb/8 workgroups
-// take that range with stride S, so at any moment an XCD works on S adjacent items (which
-// share 128-B lines) -- speed only, any placement is correct.
-struct Range {
-  int first, stride, count;
-};
-__device__ __forceinline__ Range persistent_range(int b, int nb, int n) {
-  Range r;
-  if ((nb & 7) == 0 && (n & 7) == 0 && nb <= n) {
-    const int S = nb >> 3, x = b & 7, s = b >> 3, per = n >> 3;
-    r.first = x * per + s;
-    r.stride = S;
-    r.count = s < per ? (per - s + S - 1) / S : 0;
-  } else {
-    r.first = b;
-    r.stride = nb;
-    r.count = b < n ? (n - b + nb - 1) / nb : 0;
-  }
-  return r;
-}
 
 // ---------------------------------------------------------------------------------------
 // Pass 1: rows, real -> packed half spectrum, column-major output H[m][y].
@@ -484,19 +160,6 @@ __device__ __forceinline__ double2 sym_apply(double2 v, double d, double d2, dou
   }
   if (mirror) return make_double2(0.5 * (x / d + x / d2), 0.5 * (y / d + y / d2));
   return make_double2(x / d, y / d);
-}
-
-// After the forward transform's last stage a thread holds elements (j_b + r*NS), the same
-// set the inverse transform's stage 0 reads (tid + T*r'), in a different register order:
-// r' = b + (16/R_last)*r.  fwd_to_inv permutes the registers accordingly.
-template <int M>
-__device__ __forceinline__ void fwd_to_inv(const double2 (&a)[16], double2 (&v)[16]) {
-  using P = Plan<M>;
-  constexpr int RL = P::radix(P::NSTAGES - 1);
-#pragma unroll
-  for (int b = 0; b < 16 / RL; ++b)
-#pragma unroll
-    for (int r = 0; r < RL; ++r) v[b + (16 / RL) * r] = a[b * RL + r];
 }
 
 // Element y of a column: rows are stored in segments of 2^rl_log2 (one per source rank of
@@ -713,14 +376,20 @@ constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 // Row lengths nx = 1024..16384 (half-length L = 512..8192 in one workgroup's LDS), column
 // lengths ny = 1024..8192, powers of two; `rows` (this GPU's rows) a multiple of the row
 // pass's rows per work item (<= 8).
+bool fused_rows_supported(int nx, int rows) {
+  return pow2(nx) && nx >= 1024 && nx <= 16384 && rows >= 8 && rows % 8 == 0;
+}
+
 bool fused_poisson_supported(int nx, int ny, int rows) {
   return pow2(nx) && pow2(ny) && nx >= 1024 && nx <= 16384 && ny >= 1024 && ny <= 8192 &&
          rows >= 8 && rows % 8 == 0 && ny % rows == 0;
 }
 
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  if (!fused_poisson_supported(a.nx, a.ny, a.rows) || a.kb < 1 || (1 << a.rl_log2) > a.ny)
-    throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
+  const bool ok = pass == 1 ? fused_poisson_supported(a.nx, a.ny, a.rows) && a.kb >= 1 &&
+                                 (1 << a.rl_log2) <= a.ny
+                           : fused_rows_supported(a.nx, a.rows);
+  if (!ok) throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
   if (pass == 1) {
     switch (a.ny) {
       case 1024: launch_cols<1024>(a, st); break;

@@ -8,7 +8,9 @@ import numpy as np
 from . import _lib
 from ._lib import check, dptr
 
-_PATHS = {"auto": _lib.POISSON_AUTO, "rocfft": _lib.POISSON_ROCFFT, "fused": _lib.POISSON_FUSED}
+_PATHS = {"auto": _lib.POISSON_AUTO, "rocfft": _lib.POISSON_ROCFFT, "fused": _lib.POISSON_FUSED,
+          "schur": _lib.POISSON_SCHUR}
+_PATH_NAMES = {v: k for k, v in _PATHS.items()}
 
 
 class PoissonFFT:
@@ -46,7 +48,7 @@ class PoissonFFT:
         check(_lib.load().cfdj_fps_set_poisson(self._h, _PATHS[path]), "cfdj_fps_set_poisson")
 
     def poisson(self):
-        return {_lib.POISSON_FUSED: "fused", _lib.POISSON_ROCFFT: "rocfft"}[
+        return _PATH_NAMES[
             _lib.load().cfdj_fps_get_poisson(self._h)]
 
     def solve_device(self, f_ptr, s_ptr):
@@ -173,7 +175,7 @@ class VortexMerger:
         check(_lib.load().cfdj_vm_set_poisson(self._h, _PATHS[path]), "cfdj_vm_set_poisson")
 
     def poisson(self):
-        return {_lib.POISSON_FUSED: "fused", _lib.POISSON_ROCFFT: "rocfft"}[
+        return _PATH_NAMES[
             _lib.load().cfdj_vm_get_poisson(self._h)]
 
     def field_device_ptr(self):

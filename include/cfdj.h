@@ -47,7 +47,13 @@ extern "C" {
 #define CFDJ_POISSON_AUTO 0   /* fused where supported, rocFFT otherwise (default) */
 #define CFDJ_POISSON_ROCFFT 1 /* rocFFT D2Z + divide kernel + rocFFT Z2D */
 #define CFDJ_POISSON_FUSED 2  /* hand-written 3-pass FFT: power-of-two nx 1024..16384,
-                                 ny 1024..8192, power-of-two rank counts */
+                                 ny 1024..8192, power-of-two rank counts (on y-slabs:
+                                 all-to-all transposes of the half spectrum) */
+#define CFDJ_POISSON_SCHUR 3  /* y-slabs only: hand-written row FFTs + substructured y-solve
+                                 (DST-I interiors, P x P separator system; two all-gathers
+                                 of 64 B per x-mode instead of transposes); square
+                                 power-of-two grids, 512..4096 rows per rank.  AUTO on
+                                 y-slabs picks it where supported. */
 
 /* Poisson symbol (cfdj_fps_set_symbol). */
 #define CFDJ_SYMBOL_FD 0       /* Common.jl:119-121 / fft_p.jl:37-39: aa + bb cos kx + cc cos ky */
@@ -120,7 +126,7 @@ int cfdj_vm_step_async(cfdj_vm* h, double dt, int nsteps);
 int cfdj_vm_sync(cfdj_vm* h);
 /* One vm_rhs (Common.jl:132-182) on a ghosted host array w: writes r[2:nx+1,2:ny+1]
  * (ldr >= nx+2) and the whole ghosted s (lds >= nx+2, ghost order Common.jl:138-146).
- * Single-GPU handles only. */
+ * Single-GPU and virtual-slab handles (not RCCL ranks). */
 int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, double* s,
                 long lds);
 /* Per-kernel-category device time (HIP events on the handle's stream).  enable != 0

@@ -313,7 +313,7 @@ def test_gpu_poisson_path_selection(cfdj):
         with pytest.raises(cfdj.ArgumentError):
             h.set_poisson("fused")
     with cfdj.VortexMerger(1024, 1024, dx, dy, 1000.0, kind="virtual", nranks=2) as h:
-        assert h.poisson() == "fused"  # y-slabs use the fused passes too (test_gpu_slab_fused)
+        assert h.poisson() == "schur"  # y-slabs: substructured solve (test_gpu_schur)
 
 
 def test_gpu_graph_timing_many_steps(cfdj):

@@ -13,7 +13,8 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("n,steps,path", [(64, 5, "rocfft"), (256, 5, "rocfft"),
-                                          (1024, 3, "fused"), (1024, 3, "rocfft")])
+                                          (1024, 3, "fused"), (1024, 3, "rocfft"),
+                                          (1024, 3, "schur")])
 def test_gpu_rccl_one_rank_slab(monkeypatch, n, steps, path):
     from cfd_julia_amd import VortexMerger, _lib
 

@@ -87,6 +87,7 @@ def test_gpu_fused_virtual_slabs_vs_oracle(cfdj, P, nx, ny, steps):
     dt = 5e-4 * (4096 / nx) ** 2
     ref = vo.numerical(w0, steps, dt, dx, dy, 1000.0)
     with cfdj.VortexMerger(nx, ny, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+        h.set_poisson("fused")  # the transpose path (AUTO prefers "schur" where it applies)
         assert h.poisson() == "fused"
         h.upload_interior(w0)
         h.step(dt, steps)
