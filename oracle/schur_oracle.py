@@ -80,48 +80,63 @@ def _dst_solve(rhs, lam):
     return sfft.idst(sfft.dst(rhs, type=1, axis=1) / lam, type=1, axis=1)
 
 
+def interior_lambda(c):
+    ms = np.arange(1, len(c["d"]) - 1)
+    kk = np.arange(1, c["n"] + 1)
+    return ms, c["d"][ms][:, None] + c["cc"] * np.cos(np.pi * kk / c["rl"])[None, :]
+
+
+def column_solve(col, c, m, eps=1e-6):
+    """x-mode m in {0, nx/2}: the gathered full column, FFT along y, reference symbol."""
+    ny = col.size
+    ky = vo.cos_table(vo.kx_table(2 * (len(c["d"]) - 1), eps))[:ny]
+    z = np.fft.fft(col)
+    if m == 0:
+        z[0] = 0.0  # e[1,1] = 0 (Common.jl:118)
+    den = (c["aa"] + c["bb"] * c["cx"][m]) + c["cc"] * ky
+    return np.fft.ifft(vo._cdiv_real(z, den))
+
+
+def slab_traces(blk, lam):
+    """Pass 0 of one slab (x-modes 1..L-1 as rows of `blk`): separator row, interior traces of
+    the zero-Dirichlet solve, column sum -> (4, L-1)."""
+    psi0 = _dst_solve(blk[:, 1:], lam)
+    return np.stack([blk[:, 0], psi0[:, 0], psi0[:, -1], blk.sum(axis=1)])
+
+
+def slab_solve(blk, lam, T, rank, c, ms, dy, ny):
+    """Pass 1 of slab `rank` given the traces T[q] of every rank: separator values from the
+    circulant inverse, interior solve with them as Dirichlet data, constant-mode fix."""
+    P = len(T)
+    dy2 = dy * dy
+    rhs = np.stack([T[q][0] - (T[(q - 1) % P][2] + T[q][1]) / dy2 for q in range(P)])
+    minv = c["minv"][ms]  # (L-1, P, P)
+    sp = np.einsum("mq,qm->m", minv[:, rank, :], rhs)
+    sq = np.einsum("mq,qm->m", minv[:, (rank + 1) % P, :], rhs)
+    fbar = sum(T[q][3] for q in range(P)) / ny
+    r = blk[:, 1:].copy()
+    r[:, 0] -= sp / dy2
+    r[:, -1] -= sq / dy2
+    psi = np.empty_like(blk)
+    psi[:, 0] = sp
+    psi[:, 1:] = _dst_solve(r, lam)
+    return psi + (fbar * c["corr"][ms])[:, None]
+
+
 def schur_fps(f, dx, dy, P, eps=1e-6):
     """Decomposed solve of vm_oracle.fps(f, dx, dy) on P y-slabs (single process)."""
     nx, ny = f.shape
     if nx != ny:
         raise ValueError("substructured y-solve needs nx == ny (see module docstring)")
     c = mode_constants(nx, ny, dx, dy, P, eps)
-    rl, n = c["rl"], c["n"]
+    rl = c["rl"]
     F = np.fft.rfft(f, axis=0)  # F[m, y], m = 0..nx/2
     out = np.empty_like(F)
-    # modes 0 and nx/2: full y-FFT with the reference symbol (the gathered column)
-    ky = vo.cos_table(vo.kx_table(nx, eps))[:ny]
     for m in (0, nx // 2):
-        col = np.fft.fft(F[m, :])
-        if m == 0:
-            col[0] = 0.0  # e[1,1] = 0 (Common.jl:118)
-        den = (c["aa"] + c["bb"] * c["cx"][m]) + c["cc"] * ky
-        out[m, :] = np.fft.ifft(vo._cdiv_real(col, den))
-    ms = np.arange(1, nx // 2)
-    d = c["d"][ms]
-    kk = np.arange(1, n + 1)
-    lam = d[:, None] + c["cc"] * np.cos(np.pi * kk / rl)[None, :]
-    dy2 = dy * dy
-    # pass A: interior traces with zero boundaries; separator right-hand sides
-    t1 = np.empty((P, ms.size), complex)
-    tn = np.empty((P, ms.size), complex)
-    fs = np.empty((P, ms.size), complex)
+        out[m, :] = column_solve(F[m, :], c, m, eps)
+    ms, lam = interior_lambda(c)
+    blks = [F[ms, p * rl:(p + 1) * rl] for p in range(P)]
+    T = [slab_traces(b, lam) for b in blks]
     for p in range(P):
-        blk = F[ms, p * rl:(p + 1) * rl]
-        psi0 = _dst_solve(blk[:, 1:], lam)
-        t1[p], tn[p], fs[p] = psi0[:, 0], psi0[:, -1], blk[:, 0]
-    rhs = fs - (np.roll(tn, 1, axis=0) + t1) / dy2  # tn[p-1] + t1[p]
-    s = np.einsum("mpq,qm->pm", c["minv"][ms], rhs)
-    fbar = F[ms, :].mean(axis=1)
-    # pass B: interior with the separator values as Dirichlet data, + constant-mode fix
-    for p in range(P):
-        blk = F[ms, p * rl:(p + 1) * rl].copy()
-        sp, sq = s[p], s[(p + 1) % P]
-        r = blk[:, 1:]
-        r[:, 0] -= sp / dy2
-        r[:, -1] -= sq / dy2
-        psi = np.empty_like(blk)
-        psi[:, 0] = sp
-        psi[:, 1:] = _dst_solve(r, lam)
-        out[ms, p * rl:(p + 1) * rl] = psi + (fbar * c["corr"][ms])[:, None]
+        out[ms, p * rl:(p + 1) * rl] = slab_solve(blks[p], lam, T, p, c, ms, dy, ny)
     return np.fft.irfft(out, n=nx, axis=0)

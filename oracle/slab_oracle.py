@@ -31,6 +31,10 @@ class LocalComm:
         P = self.P
         return {q: [chunks[p][q] for p in range(P)] for q in range(P)}
 
+    def allgather(self, parts):
+        # parts[p] (rank p's array) -> [parts[0], ..., parts[P-1]]
+        return [parts[p] for p in range(self.P)]
+
 
 class DistComm:
     """One rank of a torch.distributed process group (gloo on CPU)."""
@@ -51,6 +55,14 @@ class DistComm:
         self.dist.all_to_all_single(recv.view(-1), send.view(-1))
         arr = recv.numpy().view(np.complex128).reshape((self.P,) + shape)
         return {self.rank: [arr[p] for p in range(self.P)]}
+
+    def allgather(self, parts):
+        import torch
+        mine = np.ascontiguousarray(parts[self.rank])
+        t = torch.from_numpy(mine.view(np.float64).copy())
+        out = [torch.empty_like(t) for _ in range(self.P)]
+        self.dist.all_gather(out, t)
+        return [o.numpy().view(np.complex128).reshape(mine.shape) for o in out]
 
     def halo(self, slabs):
         import torch
@@ -141,6 +153,35 @@ def slab_poisson_all(w_slabs, nx, ny, dx, dy, eps, comm, neg=True, workers=1):
     return out
 
 
+def slab_poisson_schur(w_slabs, nx, ny, dx, dy, eps, comm, neg=True, workers=1):
+    """The substructured y-slab solve (cfdj_vm::poisson_schur, schur.hip): per rank, row
+    r2c; all-gather of the x-mode 0 / nx/2 columns (solved by a full y-FFT with the
+    reference symbol) and of 4 trace numbers per other x-mode; separator + interior solves;
+    row c2r.  Square grids only (oracle/schur_oracle.py)."""
+    from . import schur_oracle as so
+
+    P = comm.P
+    rows = ny // P
+    L = nx // 2
+    ranks = getattr(comm, "local_ranks", list(range(P)))
+    c = so.mode_constants(nx, ny, dx, dy, P, eps)
+    ms, lam = so.interior_lambda(c)
+    sgn = -1.0 if neg else 1.0
+    F = {p: sfft.rfft(sgn * w_slabs[i], axis=0, workers=workers) for i, p in enumerate(ranks)}
+    cols = comm.allgather({p: np.stack([F[p][0], F[p][L]]) for p in ranks})
+    G = np.concatenate(cols, axis=1)
+    g0, gL = so.column_solve(G[0], c, 0, eps), so.column_solve(G[1], c, L, eps)
+    T = comm.allgather({p: so.slab_traces(F[p][ms], lam) for p in ranks})
+    out = []
+    for p in ranks:
+        X = np.empty_like(F[p])
+        X[0] = g0[p * rows:(p + 1) * rows]
+        X[L] = gL[p * rows:(p + 1) * rows]
+        X[ms] = so.slab_solve(F[p][ms], lam, T, p, c, ms, dy, ny)
+        out.append(sfft.irfft(X, n=nx, axis=0, workers=workers))
+    return out
+
+
 def halo_rows(slabs, comm):
     """(lo, hi) ghost rows per local rank: lo = last row of p-1, hi = first row of p+1."""
     if hasattr(comm, "halo"):
@@ -160,9 +201,11 @@ def slab_rhs(w_slabs, psi_slabs, dx, dy, re, comm):
     return out
 
 
-def slab_rk3_step(wn, dt, nx, ny, dx, dy, re, eps, comm):
+def slab_rk3_step(wn, dt, nx, ny, dx, dy, re, eps, comm, poisson="transpose"):
+    solve = slab_poisson_schur if poisson == "schur" else slab_poisson_all
+
     def rhs(w):
-        return slab_rhs(w, slab_poisson_all(w, nx, ny, dx, dy, eps, comm), dx, dy, re, comm)
+        return slab_rhs(w, solve(w, nx, ny, dx, dy, eps, comm), dx, dy, re, comm)
 
     r = rhs(wn)
     wt = [a + dt * b for a, b in zip(wn, r)]

@@ -18,7 +18,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, ws, port, nx, nsteps, q):
+def _worker(rank, ws, port, nx, nsteps, q, poisson="transpose"):
     import torch.distributed as dist
 
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -34,7 +34,8 @@ def _worker(rank, ws, port, nx, nsteps, q):
         comm = so.DistComm()
         mine = [so.split(w, ws)[rank]]
         for _ in range(nsteps):
-            mine = so.slab_rk3_step(mine, 0.01, nx, ny, dx, dy, 1000.0, 1e-6, comm)
+            mine = so.slab_rk3_step(mine, 0.01, nx, ny, dx, dy, 1000.0, 1e-6, comm,
+                                    poisson=poisson)
         # gather the slabs on rank 0 and compare with the single-domain oracle
         import torch
 
@@ -58,6 +59,45 @@ def test_slab_decomposition_matches_single_domain(ws, nx):
                        join=True)
     err = q.get(timeout=5)
     assert err < 1e-13, err
+
+
+@pytest.mark.parametrize("ws,nx", [(2, 64), (4, 64)])
+def test_schur_slab_decomposition_matches_single_domain(ws, nx):
+    # the substructured solve (all-gathers only) over real process groups
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    mp.start_processes(_worker, args=(ws, port, nx, 3, q, "schur"), nprocs=ws,
+                       start_method="spawn", join=True)
+    err = q.get(timeout=5)
+    assert err < 1e-13, err
+
+
+def test_schur_oracle_matches_fps():
+    from oracle import schur_oracle as sc
+    from oracle import vm_oracle as vo
+
+    for n in (64, 256):
+        dx, dy, x, y = vo.vm_grid(n, n)
+        f = -(vo.vm_ic(n, n, x, y) + 0.01 * np.random.default_rng(n).standard_normal((n, n)))
+        ref = vo.fps(f, dx, dy)
+        for P in (1, 2, 4, 8):
+            s = sc.schur_fps(f, dx, dy, P)
+            assert np.abs(s - ref).max() < 1e-13 * np.abs(ref).max(), (n, P)
+
+
+def test_schur_local_comm_matches_single_process():
+    from oracle import schur_oracle as sc
+    from oracle import slab_oracle as so
+    from oracle import vm_oracle as vo
+
+    n, P = 128, 4
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w = vo.vm_ic(n, n, x, y)
+    a = np.concatenate(so.slab_poisson_schur(so.split(w, P), n, n, dx, dy, 1e-6,
+                                             so.LocalComm(P)), axis=1)
+    b = sc.schur_fps(-w, dx, dy, P)
+    assert np.abs(a - b).max() < 1e-15 * np.abs(b).max() * 10
 
 
 def test_slab_local_comm_many_ranks():
