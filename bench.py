@@ -8,10 +8,11 @@
 One "step" = one full RK3 step (3 RHS evaluations = 3 FFT Poisson solves + 3 fused
 Arakawa/Laplacian/RK stage kernels) over the whole grid, all data resident in HBM.
 N = 1 runs BASELINE.json config 3 (4096^2, re = 1000, dt = 5e-4: the reference's dt = .01
-is unstable at this size).  N > 1 is weak scaling on y-slabs with exactly
-4096^2 cells per GPU: 8192x4096 (N=2), 8192^2 (N=4, BASELINE config 5), 16384x8192 (N=8)
--- power-of-two sides so every rank runs the hand-written FFT passes, ny <= nx as the
-reference's ky = kx table requires (Common.jl:113).  RCCL halos + all-to-all.
+is unstable at this size).  N > 1 runs y-slabs of square power-of-two
+grids -- 8192^2 (N=2, N=4: BASELINE config 5), 16384^2 (N=8) -- i.e. 16.8 M or 33.6 M cells
+per GPU ("weak": the per-GPU work does not shrink with N; config.cells_per_gpu says how
+much).  Each RK3 stage: RCCL halo rows + the substructured Poisson solve (two all-gathers
+of O(nx) numbers) -- no spectrum transpose.
 
 Rehearsals on one GPU (not the headline): --virtual P runs the y-slab code with P virtual
 ranks (device copies for the transposes); --dist runs the RCCL slab code with a one-rank
@@ -36,7 +37,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Poisson 32 per solve (D2Z read 8 + write ~8, Z2D read ~8 + write 8; divide fused).
 STAGE_BYTES_PER_CELL_STEP = 24 + 32 + 32
 STEP_BYTES_PER_CELL = 184
-WEAK_LADDER = {1: (4096, 4096), 2: (8192, 4096), 4: (8192, 8192), 8: (16384, 8192),
+# Square power-of-two grids: the substructured y-slab Poisson solve (schur.hip) needs
+# nx == ny (the reference's ky = kx table is the periodic y-symbol only then) and every
+# rank runs the hand-written row FFTs.  Cells per GPU: 16.8 M, 33.6 M, 16.8 M, 33.6 M.
+WEAK_LADDER = {1: (4096, 4096), 2: (8192, 8192), 4: (8192, 8192), 8: (16384, 16384),
                16: (16384, 16384)}
 
 
@@ -250,7 +254,8 @@ def main():
         "data": "synthetic: vm_ic two-Gaussian vortex-merger IC (Common.jl:208-219)",
         "config": {"workload": f"NS2D vortex merger {nx}x{ny} periodic, Arakawa + FD-FFT "
                                f"Poisson + SSP-RK3 (vm.jl)", "nx": nx, "ny": ny, "dt": dt,
-                   "re": re, "parallelism": parallelism, "poisson": h.poisson()},
+                   "re": re, "parallelism": parallelism, "poisson": h.poisson(),
+                   "cells_per_gpu": cells // n_gpus},
         "ms_per_step_instrumented": round(elapsed_i * 1e3 / args.steps, 4) if elapsed_i else None,
         "achieved_hbm_gbs_step": round(step_gbs, 1),
         "step_roofline_frac": round(step_gbs / HBM_PEAK_GBS, 4),

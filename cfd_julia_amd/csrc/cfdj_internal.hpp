@@ -158,6 +158,7 @@ struct SchurArgs {
   const double* q;      // q_k = 1 - cos(pi k / rl), k <= rl
   const double* cinv;   // [L][P] first row of the inverse circulant separator system
   const double* corr;   // [L] 1/D_ref(m, 0) - 1/e_m (the reference's ky[1] = eps)
+  const double* g;      // [L][rl + 1] interior homogeneous solution gL (gL(0)=1, gL(rl)=0)
   const double2* tw;    // exp(-2 pi i k / (2 rl)), k < 2 rl
   double cc, inv_dy2, out_scale, inv_ny;
   int rl, L, P, rank;

@@ -296,7 +296,7 @@ struct Fused {
 struct SchurTables {
   int rl = 0, L = 0, P = 0;
   double cc = 0, inv_dy2 = 0;
-  double *e = nullptr, *q = nullptr, *cinv = nullptr, *corr = nullptr;
+  double *e = nullptr, *q = nullptr, *cinv = nullptr, *corr = nullptr, *g = nullptr;
   double2* tw = nullptr;
   bool ready() const { return e != nullptr; }
   void init(int nx, int ny, double dx, double dy, double eps, int nranks) {
@@ -312,6 +312,7 @@ struct SchurTables {
     const std::vector<double> kx = kx_table(nx, eps);
     const double ce = std::cos(kx[0]);  // reference cos(ky[1]) = cos(eps)
     std::vector<double> he(L), hq(rl + 1), hc((size_t)L * P, 0.0), hr(L, 0.0);
+    std::vector<double> hg((size_t)L * (rl + 1), 0.0);
     std::vector<ld> s2(rl), qk(rl + 1);
     for (int k = 0; k <= rl; ++k) {
       const ld sn = sinl(pi * (ld)k / (ld)(2 * rl));
@@ -346,11 +347,21 @@ struct SchurTables {
       }
       const double dref = (aa + bb * std::cos(kx[m])) + cc * ce;  // reference D(m, 0)
       hr[m] = (double)(1.0L / (ld)dref - 1.0L / em);
+      // gL(j) = sinh((rl-j) th) / sinh(rl th), cosh th = 1 + x, x = -e_m dy^2 / 2 (>= 0),
+      // in the overflow-free form e^{-j th} expm1(-2(rl-j) th) / expm1(-2 rl th)
+      const ld x = -em * ((ld)dy * (ld)dy) / 2.0L;
+      const ld th = log1pl(x + sqrtl(x * (x + 2.0L)));
+      const ld den = expm1l(-2.0L * rl * th);
+      for (int j = 0; j <= rl; ++j)
+        hg[(size_t)m * (rl + 1) + j] =
+            (double)(expl(-(ld)j * th) * (expm1l(-2.0L * (ld)(rl - j) * th) / den));
     }
     e = dalloc<double>(L);
     q = dalloc<double>(rl + 1);
     cinv = dalloc<double>((size_t)L * P);
     corr = dalloc<double>(L);
+    g = dalloc<double>(hg.size());
+    CFDJ_HIP(hipMemcpy(g, hg.data(), hg.size() * sizeof(double), hipMemcpyHostToDevice));
     CFDJ_HIP(hipMemcpy(e, he.data(), L * sizeof(double), hipMemcpyHostToDevice));
     CFDJ_HIP(hipMemcpy(q, hq.data(), (rl + 1) * sizeof(double), hipMemcpyHostToDevice));
     CFDJ_HIP(hipMemcpy(cinv, hc.data(), hc.size() * sizeof(double), hipMemcpyHostToDevice));
@@ -362,8 +373,9 @@ struct SchurTables {
     dfree(q);
     dfree(cinv);
     dfree(corr);
+    dfree(g);
     dfree(tw);
-    e = q = cinv = corr = nullptr;
+    e = q = cinv = corr = g = nullptr;
     tw = nullptr;
   }
   SchurArgs args(double2* H, double2* T, int rank, double out_scale, int ny) const {
@@ -374,6 +386,7 @@ struct SchurTables {
     a.q = q;
     a.cinv = cinv;
     a.corr = corr;
+    a.g = g;
     a.tw = tw;
     a.cc = cc;
     a.inv_dy2 = inv_dy2;

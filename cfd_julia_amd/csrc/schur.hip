@@ -7,13 +7,14 @@
 // D(m, k), except at k = 0 where the reference's ky[1] = eps shifts the constant mode (a
 // rank-one correction, `corr`).  Instead of transposing the whole spectrum between GPUs
 // (two all-to-alls of nx*ny/2 complex per solve), every slab
-//   pass 0 (schur_trace_kernel): solves its interior rows 1..rl-1 with zero Dirichlet data
-//          (DST-I = FFT of length 2 rl on the odd extension, in LDS) and keeps only the two
-//          boundary values of that solution, its separator row f[0] and its column sum;
+//   pass 0 (schur_trace_kernel): the two boundary values of its interior rows' solution with
+//          zero Dirichlet data (dot products with the tabulated interior Green's function),
+//          its separator row f[0] and its column sum;
 //   (the host all-gathers those 4 numbers per mode: 64 B x nx/2 per rank)
 //   pass 1 (schur_solve_kernel): solves the P x P circulant separator system for its two
-//          separator values (precomputed inverse), re-solves the interior with them as
-//          Dirichlet data and writes psi-hat (plus the constant-mode correction) in place.
+//          separator values (precomputed inverse), solves the interior rows 1..rl-1 with
+//          them as Dirichlet data (DST-I = FFT of length 2 rl on the odd extension, in LDS)
+//          and writes psi-hat (plus the constant-mode correction) in place.
 // The x-modes 0 and nx/2 (packed in column 0) are solved separately: the column is gathered
 // and FFT'd along y with the reference symbol (packed_divide_kernel).
 // Host-side tables (long double): e_m, q_k, the circulant inverse, corr -- host_common.hpp.
@@ -101,45 +102,32 @@ __device__ __forceinline__ double2 dst_divide(double2 y, int k, double em, doubl
   return make_double2(y.x / lam, y.y / lam);
 }
 
-template <int M2>
-__global__ __launch_bounds__(Plan<M2>::T) void schur_trace_kernel(const SchurArgs a) {
-  using P = Plan<M2>;
-  constexpr int RL = M2 / 2;
-  __shared__ double2 lds[P::PAD];
-  const TwGlobal<M2> tw{a.tw};
-  const int tid = threadIdx.x;
+// Pass 0: one workgroup per x-mode.  The zero-Dirichlet interior solution's boundary values
+// are rows of the interior Green's function, (T_int^-1)[1, j] = -dy^2 gL(j) and
+// (T_int^-1)[n, j] = -dy^2 gL(rl - j) (gL: the homogeneous solution with gL(0) = 1,
+// gL(rl) = 0, tabulated on the host in long double), so the traces are two dot products
+// over the slab column -- one streaming read, no transform.
+constexpr int kTraceThreads = 256;
+__global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurArgs a) {
   const int m = 1 + xcd_remap(blockIdx.x, gridDim.x);
-  const double2* col = a.H + (size_t)m * RL;
-  const double2 zero = make_double2(0.0, 0.0);
-
-  double2 v[16];
-  double2 fs = zero;
-  load_odd<M2>(v, col, tid, zero, zero, fs);
-  stage_regs<M2, 0, -1>(v, tid, tw);
-  lds_write<M2, 0>(lds, v, tid);
-  __syncthreads();
-  run_stages<M2, 1, -1, false>(lds, v, tid, tw);
-  double2 w[16];
-  fwd_to_inv<M2>(v, w);  // w[r] = Y at k = tid + T r
-  const double em = a.e[m];
-  double2 t1 = zero, tn = zero;
-#pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int k = tid + P::T * r;
-    const double2 W = dst_divide<M2>(w[r], k, em, a.cc, a.q);
-    const double2 c = tw.w(k);  // exp(-i pi k / RL)
-    // psi_1 = sum W_k e^{+i pi k/RL} / M2;  psi_{RL-1} = sum W_k (-1)^k e^{-i pi k/RL} / M2
-    t1 = cadd(t1, cmul(W, cconj(c)));
-    const double2 u = cmul(W, c);
-    tn = (k & 1) ? csub(tn, u) : cadd(tn, u);
+  const int rl = a.rl;
+  const double2* col = a.H + (size_t)m * rl;
+  const double* g = a.g + (size_t)m * (rl + 1);
+  double2 t1 = make_double2(0.0, 0.0), tn = t1, fs = t1;
+  for (int j = 1 + threadIdx.x; j < rl; j += kTraceThreads) {
+    const double2 f = col[j];
+    t1 = cadd(t1, cscale(f, g[j]));
+    tn = cadd(tn, cscale(f, g[rl - j]));
+    fs = cadd(fs, f);
   }
-  block_sum3<P::T>(t1, tn, fs);
-  if (tid == 0) {
+  block_sum3<kTraceThreads>(t1, tn, fs);
+  if (threadIdx.x == 0) {
     const double2 fsep = col[0];
+    const double mdy2 = -1.0 / a.inv_dy2;
     double2* out = a.T + ((size_t)a.rank * a.L + m) * 4;
     out[0] = fsep;
-    out[1] = cscale(t1, 1.0 / M2);
-    out[2] = cscale(tn, 1.0 / M2);
+    out[1] = cscale(t1, mdy2);
+    out[2] = cscale(tn, mdy2);
     out[3] = cadd(fs, fsep);
   }
 }
@@ -231,7 +219,7 @@ template <int M2>
 void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
   const dim3 grid(a.L - 1), block(Plan<M2>::T);
   if (pass == 0)
-    hipLaunchKernelGGL(schur_trace_kernel<M2>, grid, block, 0, st, a);
+    hipLaunchKernelGGL(schur_trace_kernel, grid, dim3(kTraceThreads), 0, st, a);
   else
     hipLaunchKernelGGL(schur_solve_kernel<M2>, grid, block, 0, st, a);
 }
