@@ -37,6 +37,11 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 # Poisson 32 per solve (D2Z read 8 + write ~8, Z2D read ~8 + write 8; divide fused).
 STAGE_BYTES_PER_CELL_STEP = 24 + 32 + 32
 STEP_BYTES_PER_CELL = 184
+# per-kernel algorithmic bytes per cell for cfdj_vm_kernel_bench ids:
+# stages read w (+ wn) and psi and write the stage output; each fused Poisson pass reads
+# and writes 8 B per cell (real field or half spectrum)
+KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16}
+KB_LAUNCHES = 20
 # Square power-of-two grids: the substructured y-slab Poisson solve (schur.hip) needs
 # nx == ny (the reference's ky = kx table is the periodic y-symbol only then) and every
 # rank runs the hand-written row FFTs.  Cells per GPU: 16.8 M, 33.6 M, 16.8 M, 33.6 M.
@@ -204,6 +209,19 @@ def main():
     # sanity: the state stays finite and bounded (conservative scheme)
     h.set_check_finite(True)
     h.sync()
+    h.set_check_finite(False)
+
+    # (3) per-kernel roofline: each kernel of the step launched KB_LAUNCHES times back to
+    # back between two HIP events on the handle's stream (runs after (1)/(2): it clobbers
+    # the stage buffers).  Single-GPU fused path only; slab runs use (2)'s events.
+    kb = {}
+    if n_gpus == 1 and not args.virtual and not args.dist and h.poisson() == "fused":
+        for kid, name in _lib.KB_NAMES.items():
+            us = h.kernel_bench(kid, dt, KB_LAUNCHES) * 1e3
+            alg = KB_BYTES_PER_CELL[kid] * nx * ny
+            kb[name] = {"us_per_launch": round(us, 2), "alg_bytes": alg,
+                        "alg_gbs": round(alg / (us * 1e-6) / 1e9, 1),
+                        "frac": round(alg / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
 
     parallelism = "single" if n_gpus == 1 else f"yslab{n_gpus}"
     if args.virtual:
@@ -214,9 +232,22 @@ def main():
     value = cells * args.steps / elapsed / 1e6
     ms_step = elapsed * 1e3 / max(args.steps, 1)
     local_cells = cells / n_gpus
-    stage_ms, stage_n = kern["stage"]
-    stage_alg_bytes = STAGE_BYTES_PER_CELL_STEP * local_cells * args.steps
-    stage_gbs = stage_alg_bytes / (stage_ms * 1e-3) / 1e9 if stage_ms > 0 else None
+    if kb:
+        # the three stage kernels together: algorithmic bytes 24 + 32 + 32 per cell over
+        # their summed per-launch times
+        st = [kb[f"vm_stage_kernel<{i}>"] for i in (1, 2, 3)]
+        stage_us = sum(k["us_per_launch"] for k in st) / 3.0
+        stage_alg = sum(k["alg_bytes"] for k in st) / 3.0
+        stage_n = 3 * KB_LAUNCHES
+        source = (f"HIP events around {KB_LAUNCHES} back-to-back launches of each stage "
+                  f"kernel on the handle stream (cfdj_vm_kernel_bench), mean of stages 1-3")
+    else:
+        stage_ms, stage_n = kern["stage"]
+        stage_us = stage_ms * 1e3 / max(stage_n, 1)
+        stage_alg = STAGE_BYTES_PER_CELL_STEP / 3.0 * local_cells
+        source = ("HIP events around every kernel on the handle stream, over a second "
+                  "timed region of the same K steps (eager launches)")
+    stage_gbs = stage_alg / (stage_us * 1e-6) / 1e9 if stage_us > 0 else None
     roofline = {
         "kernel": "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)",
         "bound": "hbm",
@@ -225,11 +256,10 @@ def main():
         "unit": "GB/s",
         "frac": round(stage_gbs / HBM_PEAK_GBS, 4) if stage_gbs else None,
         "traffic": None,
-        "alg_bytes_per_launch": int(round(stage_alg_bytes / max(stage_n, 1))),
-        "avg_launch_us": round(stage_ms * 1e3 / max(stage_n, 1), 2),
+        "alg_bytes_per_launch": int(round(stage_alg)),
+        "avg_launch_us": round(stage_us, 2),
         "launches": stage_n,
-        "source": "HIP events around every kernel on the handle stream, over a second "
-                  "timed region of the same K steps (eager launches)",
+        "source": source,
     }
     pmc = load_pmc(nx)
     if pmc:
@@ -260,6 +290,7 @@ def main():
         "achieved_hbm_gbs_step": round(step_gbs, 1),
         "step_roofline_frac": round(step_gbs / HBM_PEAK_GBS, 4),
         "kernels": breakdown,
+        "kernel_bench": kb or None,
         "roofline": roofline,
     }
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.virtual:

@@ -21,6 +21,9 @@ ERR_NAMES = {-1: "CFDJ_ERR_ARG", -2: "CFDJ_ERR_HIP", -3: "CFDJ_ERR_ROCFFT",
              -4: "CFDJ_ERR_RCCL", -5: "CFDJ_ERR_NONFINITE", -6: "CFDJ_ERR_STATE"}
 K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
+# cfdj_vm_kernel_bench kernel ids (CFDJ_KB_*)
+KB_NAMES = {1: "vm_stage_kernel<1>", 2: "vm_stage_kernel<2>", 3: "vm_stage_kernel<3>",
+            4: "rows_fwd_kernel", 5: "cols_kernel", 6: "rows_inv_kernel"}
 POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED, POISSON_SCHUR = 0, 1, 2, 3
 SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1
 CAVITY_DST, CAVITY_MG = 0, 1
@@ -70,6 +73,7 @@ SIGNATURES = {
     "cfdj_vm_rhs": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long, _dp, C.c_long]),
     "cfdj_vm_set_timing": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_timing": (C.c_int, [_vp, _dp, _lp]),
+    "cfdj_vm_kernel_bench": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, _dp]),
     "cfdj_vm_set_check_finite": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_field_device": (C.c_int, [_vp, C.POINTER(_vp)]),
     "cfdj_vm_slab": (C.c_int, [_vp, _ip, _ip]),

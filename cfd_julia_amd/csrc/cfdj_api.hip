@@ -421,6 +421,44 @@ struct cfdj_vm {
     }
   }
 
+  // `n` back-to-back launches of ONE kernel of the step between two events on the handle's
+  // stream: the per-launch device time the roofline is priced on (bench.py).  kernel =
+  // CFDJ_KB_*; single-GPU fused handles only.  Clobbers the stage / spectrum buffers and
+  // (stage 3) advances wn -- run it after the timed regions.
+  double kernel_bench(int kernel, double dt, int n) {
+    CFDJ_REQUIRE(mode == Mode::Single && use_fused,
+                 "kernel bench needs a single-GPU handle on the fused Poisson path");
+    CFDJ_REQUIRE(kernel >= CFDJ_KB_STAGE1 && kernel <= CFDJ_KB_ROWS_INV, "bad kernel id");
+    CFDJ_REQUIRE(n >= 1, "launches must be >= 1");
+    Slab& s = slabs[0];
+    const FusedPoissonArgs a = fused.args(sym, s.wn, s.psi, spec, true);
+    hipEvent_t e[2];
+    CFDJ_HIP(hipEventCreate(&e[0]));
+    CFDJ_HIP(hipEventCreate(&e[1]));
+    float t = 0.f;
+    try {
+      CFDJ_HIP(hipEventRecord(e[0], stream));
+      for (int i = 0; i < n; ++i) {
+        switch (kernel) {
+          case CFDJ_KB_STAGE1: launch_stage(1, stage_params(s, s.wn, s.wn, s.wa, dt), stream); break;
+          case CFDJ_KB_STAGE2: launch_stage(2, stage_params(s, s.wa, s.wn, s.wb, dt), stream); break;
+          case CFDJ_KB_STAGE3: launch_stage(3, stage_params(s, s.wb, s.wn, s.wn, dt), stream); break;
+          default: launch_fused_poisson_pass(kernel - CFDJ_KB_ROWS_FWD, a, stream); break;
+        }
+      }
+      CFDJ_HIP(hipEventRecord(e[1], stream));
+      CFDJ_HIP(hipEventSynchronize(e[1]));
+      CFDJ_HIP(hipEventElapsedTime(&t, e[0], e[1]));
+    } catch (...) {
+      (void)hipEventDestroy(e[0]);
+      (void)hipEventDestroy(e[1]);
+      throw;
+    }
+    (void)hipEventDestroy(e[0]);
+    (void)hipEventDestroy(e[1]);
+    return (double)t / n;
+  }
+
   void steps_eager(double dt, int nsteps) {
     for (int n = 0; n < nsteps; ++n) {
       stage(1, dt);
@@ -896,6 +934,16 @@ int cfdj_vm_timing(cfdj_vm* h, double* ms, long* launches) {
       if (ms) ms[k] = h->ms[k];
       if (launches) launches[k] = h->launches[k];
     }
+  });
+}
+
+int cfdj_vm_kernel_bench(cfdj_vm* h, int kernel, double dt, int launches,
+                         double* ms_per_launch) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && ms_per_launch, "NULL argument");
+    select_device(h->device);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    *ms_per_launch = h->kernel_bench(kernel, dt, launches);
   });
 }
 

@@ -152,6 +152,19 @@ __device__ __forceinline__ double fd_symbol(double ax, double cc, double cy) {
   return ax + cc * cy;
 }
 
+// 1/d for the spectral divide: v_rcp_f64 refined by two Newton steps (|rel. error| below
+// 2^-52 before the final rounding), i.e. within an ulp of the correctly rounded quotient
+// the reference's `e / (...)` (Common.jl:121) forms.  Two true fp64 divisions per complex
+// element cost the column pass 15 us of 81 at 4096^2 (r02, cols_kernel variants); d is a
+// normal number here (|d| >= ~1e-7 for grids up to 16384^2, never 0 or denormal).
+__device__ __forceinline__ double recip_nr(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = __builtin_fma(-d, r, 1.0);
+  r = __builtin_fma(r, e, r);
+  e = __builtin_fma(-d, r, 1.0);
+  return __builtin_fma(r, e, r);
+}
+
 // Twiddles live in LDS as a 2-level table, W_L^e = hi[e >> 6] * lo[e & 63] (one rounding),
 // filled once per persistent workgroup from the host-built long-double tables.  Keeping
 // them out of the vector-memory stream matters: vmcnt is in order, so a twiddle load issued

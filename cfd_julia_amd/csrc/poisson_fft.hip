@@ -37,7 +37,10 @@ struct RowCfg {
   static constexpr int T = Plan<L>::T;
   // rows per work item: >= 4 (64-B column segments) where the LDS holds them, fewer for
   // the long rows of the multi-GPU grids (L = 4096: 2, L = 8192: 1 -- 136 KB per row)
-  static constexpr int XR_WANT = (256 / T) > 4 ? (256 / T) : 4;
+#ifndef CFDJ_ROWS_XR_MIN
+#define CFDJ_ROWS_XR_MIN 4
+#endif
+  static constexpr int XR_WANT = (256 / T) > CFDJ_ROWS_XR_MIN ? (256 / T) : CFDJ_ROWS_XR_MIN;
   static constexpr int XR_FIT = (140 * 1024) / (Plan<L>::ROWSTRIDE * 16);
   static constexpr int XR = XR_WANT < XR_FIT ? XR_WANT : XR_FIT;
   static_assert(XR >= 1, "row does not fit the LDS");
@@ -147,19 +150,20 @@ struct DivArgs {
   unsigned seg;   // elements between the segments of one column (y-slabs: (L/P) * rows)
 };
 
-// v / d, or v * (1/d) for the Dirichlet (DST-I) multiplier of lid_driven_cavity.jl:17, or
+// v / d as v * (1/d) (recip_nr: the divide is the column pass's costliest step), for the
+// FD symbol and for the Dirichlet (DST-I) multiplier of lid_driven_cavity.jl:17 alike; or
 // the Hermitian projection (v/d + v/d2)/2 of a symbol that is not even in ky: what
 // real(ifft(...)) keeps of a non-Hermitian quotient (Common.jl:123 with ny < nx).  The
 // sign is applied first, as divide_kernel does.
 __device__ __forceinline__ double2 sym_apply(double2 v, double d, double d2, double sgn,
-                                             bool recip, bool mirror) {
+                                             bool mirror) {
   const double x = sgn * v.x, y = sgn * v.y;
-  if (recip) {
-    const double id = 1.0 / d;
-    return make_double2(x * id, y * id);
+  const double id = recip_nr(d);
+  if (mirror) {
+    const double id2 = recip_nr(d2);
+    return make_double2(0.5 * (x * id + x * id2), 0.5 * (y * id + y * id2));
   }
-  if (mirror) return make_double2(0.5 * (x / d + x / d2), 0.5 * (y / d + y / d2));
-  return make_double2(x / d, y / d);
+  return make_double2(x * id, y * id);
 }
 
 // Element y of a column: rows are stored in segments of 2^rl_log2 (one per source rank of
@@ -178,7 +182,7 @@ __device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __rest
     for (int r = 0; r < R0; ++r) a[b * R0 + r] = col[col_off(in_pos<M, 0>(tid, b, r), rl_log2, seg)];
 }
 
-template <int M>
+template <int M, bool MIRROR>
 __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ C,
                                                         const double2* __restrict__ twM_,
                                                         const DivArgs da) {
@@ -192,7 +196,8 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
   const int ml = xcd_remap(blockIdx.x, gridDim.x);
   const int m = da.m0 + ml;  // global x-mode
   const double sgn = da.neg ? -1.0 : 1.0;
-  const bool mirror = da.cy_mirror != nullptr;
+  constexpr bool mirror = MIRROR;  // symbol not even in ky (ny < nx): a template flag, so
+                                  // the square-grid kernel carries no cy_mirror loads
   double2* col = C + ((size_t)ml << da.rl_log2);
 
   double2 a[16];
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
       const int k = tid + P::T * r;
       const double d = fd_symbol(ax, da.cc, da.cy[k]);
       const double d2 = mirror ? fd_symbol(ax, da.cc, da.cy_mirror[k]) : d;
-      const double2 q = sym_apply(v[r], d, d2, sgn, da.recip, mirror);
+      const double2 q = sym_apply(v[r], d, d2, sgn, mirror);
       v[r] = make_double2(q.x * da.scale, q.y * da.scale);
     }
   } else {
@@ -237,8 +242,8 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
       const double d0m = fd_symbol(ax, da.cc, cym);
       const double dLm = fd_symbol(axL, da.cc, cym);
       const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0 (Common.jl:118)
-                                : sym_apply(A, d0, d0m, sgn, da.recip, mirror);
-      const double2 B2 = sym_apply(B, dL, dLm, sgn, da.recip, mirror);
+                                : sym_apply(A, d0, d0m, sgn, mirror);
+      const double2 B2 = sym_apply(B, dL, dLm, sgn, mirror);
       v[r] = make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
     }
   }
@@ -366,7 +371,10 @@ template <int M>
 void launch_cols(const FusedPoissonArgs& a, hipStream_t st) {
   DivArgs da{a.cx,  a.cy,  a.cy_mirror,        a.aa, a.bb, a.cc,       a.scale,
              a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg};
-  hipLaunchKernelGGL(cols_kernel<M>, dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, a.twM, da);
+  if (a.cy_mirror == nullptr)
+    hipLaunchKernelGGL((cols_kernel<M, false>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, a.twM, da);
+  else
+    hipLaunchKernelGGL((cols_kernel<M, true>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, a.twM, da);
 }
 
 constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }

@@ -159,6 +159,14 @@ class VortexMerger:
         check(_lib.load().cfdj_vm_timing(self._h, ms, n), "cfdj_vm_timing")
         return {name: (ms[i], n[i]) for i, name in enumerate(_lib.K_NAMES)}
 
+    def kernel_bench(self, kernel, dt, launches=20):
+        """ms per launch of `launches` back-to-back launches of one kernel (CFDJ_KB_*);
+        clobbers the stage buffers and advances the field: use after the timed runs."""
+        ms = C.c_double()
+        check(_lib.load().cfdj_vm_kernel_bench(self._h, int(kernel), float(dt), int(launches),
+                                               C.byref(ms)), "cfdj_vm_kernel_bench")
+        return ms.value
+
     def set_check_finite(self, enable=True):
         check(_lib.load().cfdj_vm_set_check_finite(self._h, int(bool(enable))),
               "cfdj_vm_set_check_finite")

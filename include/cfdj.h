@@ -134,6 +134,19 @@ int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, doub
  * receive the accumulated totals (either may be NULL). */
 int cfdj_vm_set_timing(cfdj_vm* h, int enable);
 int cfdj_vm_timing(cfdj_vm* h, double* ms, long* launches);
+/* Kernel microbenchmark (no reference equivalent; bench.py's roofline): `launches`
+ * back-to-back launches of one kernel of the step between two HIP events on the handle's
+ * stream; *ms_per_launch = elapsed / launches.  Single-GPU handles on the fused Poisson
+ * path.  Overwrites the stage and spectrum buffers and (stage 3) advances the vorticity:
+ * call it after the runs whose results matter. */
+#define CFDJ_KB_STAGE1 1   /* vm_stage_kernel<1>: wn -> w1 (vm.jl:28) */
+#define CFDJ_KB_STAGE2 2   /* vm_stage_kernel<2>: (w1, wn) -> w2 (vm.jl:43-47) */
+#define CFDJ_KB_STAGE3 3   /* vm_stage_kernel<3>: (w2, wn) -> wn (vm.jl:62-66) */
+#define CFDJ_KB_ROWS_FWD 4 /* fused Poisson pass 1: row r2c FFT */
+#define CFDJ_KB_COLS 5     /* fused Poisson pass 2: column FFT + divide + inverse FFT */
+#define CFDJ_KB_ROWS_INV 6 /* fused Poisson pass 3: row c2r FFT */
+int cfdj_vm_kernel_bench(cfdj_vm* h, int kernel, double dt, int launches,
+                         double* ms_per_launch);
 /* Optional finiteness check of the vorticity after each cfdj_vm_step call. */
 int cfdj_vm_set_check_finite(cfdj_vm* h, int enable);
 /* Device pointer of this rank's nx-by-(ny/nranks) vorticity slab (pitch nx). */

@@ -245,6 +245,24 @@ def test_gpu_timing_counters(cfdj):
     assert all(v[0] > 0 for k, v in t.items() if k != "comm")
 
 
+def test_gpu_kernel_bench(cfdj):
+    """cfdj_vm_kernel_bench: every kernel id times > 0; the rocFFT path and bad ids are
+    rejected (ARG)."""
+    from cfd_julia_amd import _lib
+
+    n = 1024
+    dx, dy, w0 = vm_setup(n)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.upload_interior(w0)
+        for kid in _lib.KB_NAMES:
+            assert h.kernel_bench(kid, 1e-3, 3) > 0
+        with pytest.raises(_lib.ArgumentError):
+            h.kernel_bench(7, 1e-3, 3)
+        h.set_poisson("rocfft")
+        with pytest.raises(_lib.ArgumentError):
+            h.kernel_bench(1, 1e-3, 3)
+
+
 @pytest.mark.parametrize("rpw", [1, 3, 8, 64, 1000])
 def test_gpu_rows_per_wave_invariance(cfdj, rpw):
     n = 192
