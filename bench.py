@@ -40,7 +40,10 @@ STEP_BYTES_PER_CELL = 184
 # per-kernel algorithmic bytes per cell for cfdj_vm_kernel_bench ids:
 # stages read w (+ wn) and psi and write the stage output; each fused Poisson pass reads
 # and writes 8 B per cell (real field or half spectrum)
-KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16}
+# FFT-fused stage kernels (vm_fused.hip) read the column-pass spectrum 8 + omega_s 8
+# (+ omega^n 8) and write omega_out 8 + the next row spectrum 8; 10 = the column pass
+# writing the rotated layout they read
+KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16, 7: 32, 8: 40, 9: 40, 10: 16}
 KB_LAUNCHES = 20
 # Square power-of-two grids: the substructured y-slab Poisson solve (schur.hip) needs
 # nx == ny (the reference's ky = kx table is the periodic y-symbol only then) and every
@@ -110,6 +113,8 @@ def main():
                     help="one-GPU rehearsal: RCCL slab code with a one-rank communicator")
     ap.add_argument("--poisson", default="auto", choices=["auto", "fused", "rocfft", "schur"])
     ap.add_argument("--rows-per-wave", type=int, default=None)
+    ap.add_argument("--no-fused-stage", action="store_true",
+                    help="five-pass stage sequence instead of the FFT-fused stage kernel")
     ap.add_argument("--cpu-steps", type=int, default=2)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true",
@@ -161,6 +166,8 @@ def main():
     else:
         h = VortexMerger(nx, ny, dx, dy, re, device=local_rank)
     h.set_poisson(args.poisson)
+    if args.no_fused_stage:
+        h.set_fused_stage(False)
     if args.rows_per_wave:
         h.set_rows_per_wave(args.rows_per_wave)
 
@@ -232,10 +239,12 @@ def main():
     value = cells * args.steps / elapsed / 1e6
     ms_step = elapsed * 1e3 / max(args.steps, 1)
     local_cells = cells / n_gpus
+    fstage = h.fused_stage()
+    kname = "vm_fused_stage_kernel" if fstage else "vm_stage_kernel"
     if kb:
-        # the three stage kernels together: algorithmic bytes 24 + 32 + 32 per cell over
-        # their summed per-launch times
-        st = [kb[f"vm_stage_kernel<{i}>"] for i in (1, 2, 3)]
+        # the three stage kernels of the step together: algorithmic bytes (24 + 32 + 32 or,
+        # FFT-fused, 32 + 40 + 40 per cell) over their summed per-launch times
+        st = [kb[f"{kname}<{i}>"] for i in (1, 2, 3)]
         stage_us = sum(k["us_per_launch"] for k in st) / 3.0
         stage_alg = sum(k["alg_bytes"] for k in st) / 3.0
         stage_n = 3 * KB_LAUNCHES
@@ -244,12 +253,14 @@ def main():
     else:
         stage_ms, stage_n = kern["stage"]
         stage_us = stage_ms * 1e3 / max(stage_n, 1)
-        stage_alg = STAGE_BYTES_PER_CELL_STEP / 3.0 * local_cells
+        stage_alg = (112 if fstage else STAGE_BYTES_PER_CELL_STEP) / 3.0 * local_cells
         source = ("HIP events around every kernel on the handle stream, over a second "
                   "timed region of the same K steps (eager launches)")
     stage_gbs = stage_alg / (stage_us * 1e-6) / 1e9 if stage_us > 0 else None
     roofline = {
-        "kernel": "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)",
+        "kernel": ("vm_fused_stage_kernel (row c2r of psi-hat + Arakawa J + 5-pt Laplacian "
+                   "+ RK3 stage + row r2c of the output, psi on chip)" if fstage else
+                   "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)"),
         "bound": "hbm",
         "achieved": round(stage_gbs, 1) if stage_gbs else None,
         "peak": HBM_PEAK_GBS,
@@ -262,7 +273,7 @@ def main():
         "source": source,
     }
     pmc = load_pmc(nx)
-    if pmc:
+    if pmc and pmc.get("stage_kernel", "vm_stage_kernel") == kname:
         roofline["traffic"] = pmc["stage_bytes_per_launch"]
         roofline["traffic_source"] = pmc["source"]
     step_gbs = STEP_BYTES_PER_CELL * local_cells * args.steps / elapsed / 1e9
@@ -285,6 +296,7 @@ def main():
         "config": {"workload": f"NS2D vortex merger {nx}x{ny} periodic, Arakawa + FD-FFT "
                                f"Poisson + SSP-RK3 (vm.jl)", "nx": nx, "ny": ny, "dt": dt,
                    "re": re, "parallelism": parallelism, "poisson": h.poisson(),
+                   "fused_stage": fstage,
                    "cells_per_gpu": cells // n_gpus},
         "ms_per_step_instrumented": round(elapsed_i * 1e3 / args.steps, 4) if elapsed_i else None,
         "achieved_hbm_gbs_step": round(step_gbs, 1),

@@ -326,6 +326,29 @@ __device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[16], int t
   }
 }
 
+// run_stages for workgroups whose transform groups are not all busy: a group with
+// act == false keeps every barrier (they are workgroup-wide, and stay outside the
+// branches: act may differ inside one wavefront when T < 64) but touches no LDS.
+template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW>
+__device__ __forceinline__ void run_stages_if(double2* buf, double2 (&v)[16], int tid,
+                                              const TW& tw, bool act) {
+  using P = Plan<L>;
+  if constexpr (S < P::NSTAGES) {
+    StageTw<L, S> st;
+    if (act) {
+      st = stage_tw<L, S, TW>(tid, tw);
+      lds_read<L, S, IL>(buf, v, tid);
+    }
+    __syncthreads();
+    if (act) stage_regs<L, S, DIR>(v, st);
+    if constexpr (S + 1 < P::NSTAGES || LAST_TO_LDS) {
+      if (act) lds_write<L, S, IL>(buf, v, tid);
+      __syncthreads();
+    }
+    run_stages_if<L, S + 1, DIR, LAST_TO_LDS, IL, TW>(buf, v, tid, tw, act);
+  }
+}
+
 // After the forward transform's last stage a thread holds elements (j_b + r*NS), the same
 // set the inverse transform's stage 0 reads (tid + T*r'), in a different register order:
 // r' = b + (16/R_last)*r.  fwd_to_inv permutes the registers accordingly.

@@ -265,6 +265,8 @@ struct Fused {
     a.s = s;
     a.H = H;
     a.C = C;
+    a.Cout = nullptr;
+    a.rot = 0;
     a.kb = (nx / 2) / nranks;
     a.m0 = rank * a.kb;
     int lg = 0;

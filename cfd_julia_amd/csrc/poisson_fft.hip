@@ -148,6 +148,7 @@ struct DivArgs {
   int m0;         // global index of this buffer's first column (y-slabs: rank * L/P)
   int rl_log2;    // rows per segment (y-slabs: rows per rank; one GPU: M)
   unsigned seg;   // elements between the segments of one column (y-slabs: (L/P) * rows)
+  int rot;        // output element y goes to (y - rot) mod M (one GPU only; 0 = natural)
 };
 
 // v / d as v * (1/d) (recip_nr: the divide is the column pass's costliest step), for the
@@ -183,7 +184,8 @@ __device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __rest
 }
 
 template <int M, bool MIRROR>
-__global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ C,
+__global__ __launch_bounds__(Plan<M>::T) void cols_kernel(const double2* __restrict__ C,
+                                                        double2* __restrict__ Cout,
                                                         const double2* __restrict__ twM_,
                                                         const DivArgs da) {
   // One column per workgroup (2 resident per CU at M = 4096): not persistent, because the
@@ -198,7 +200,8 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
   const double sgn = da.neg ? -1.0 : 1.0;
   constexpr bool mirror = MIRROR;  // symbol not even in ky (ny < nx): a template flag, so
                                   // the square-grid kernel carries no cy_mirror loads
-  double2* col = C + ((size_t)ml << da.rl_log2);
+  const double2* col = C + ((size_t)ml << da.rl_log2);
+  double2* ocol = Cout + ((size_t)ml << da.rl_log2);
 
   double2 a[16];
   load_col<M>(a, col, tid, da.rl_log2, da.seg);
@@ -259,7 +262,8 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(double2* __restrict__ 
   for (int b = 0; b < 16 / RL; ++b)
 #pragma unroll
     for (int r = 0; r < RL; ++r)
-      col[col_off(out_pos<M, SL>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
+      ocol[col_off((out_pos<M, SL>(tid, b, r) - da.rot) & (M - 1), da.rl_log2, da.seg)] =
+          v[b * RL + r];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -370,11 +374,12 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
 template <int M>
 void launch_cols(const FusedPoissonArgs& a, hipStream_t st) {
   DivArgs da{a.cx,  a.cy,  a.cy_mirror,        a.aa, a.bb, a.cc,       a.scale,
-             a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg};
+             a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg, a.rot};
+  double2* out = a.Cout ? a.Cout : a.C;
   if (a.cy_mirror == nullptr)
-    hipLaunchKernelGGL((cols_kernel<M, false>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, a.twM, da);
+    hipLaunchKernelGGL((cols_kernel<M, false>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, out, a.twM, da);
   else
-    hipLaunchKernelGGL((cols_kernel<M, true>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, a.twM, da);
+    hipLaunchKernelGGL((cols_kernel<M, true>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, out, a.twM, da);
 }
 
 constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
@@ -395,7 +400,8 @@ bool fused_poisson_supported(int nx, int ny, int rows) {
 
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st) {
   const bool ok = pass == 1 ? fused_poisson_supported(a.nx, a.ny, a.rows) && a.kb >= 1 &&
-                                 (1 << a.rl_log2) <= a.ny
+                                 (1 << a.rl_log2) <= a.ny &&
+                                 (a.rot == 0 || (1 << a.rl_log2) == a.ny)
                            : fused_rows_supported(a.nx, a.rows);
   if (!ok) throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
   if (pass == 1) {
