@@ -46,7 +46,6 @@ struct FCfg {
   static constexpr int SLOT = P::ROWSTRIDE;            // complex elements per slot
   static constexpr int THREADS = XR * T;
   static constexpr int PAIRS = (L / 2) * XR / THREADS;  // (m, L-m) pairs per thread
-  static constexpr int CHUNKS = L / THREADS;            // x-pairs per thread per row
   static_assert(THREADS == 256, "one 256-thread workgroup per CU");
   static_assert(NSLOT * SLOT * 16 <= 140 * 1024, "slots must leave room for twiddles");
 };
@@ -150,12 +149,68 @@ __device__ __forceinline__ Win psi_win(const double2* row, int pp) {
   return w;
 }
 
+// omega inputs of one stencil step, loaded in one batch (no branches, so the loads issue
+// back to back and the wait is one vmcnt): wave w owns the contiguous x-pairs
+// [w L/4, (w+1) L/4), chunk c of it pairs w L/4 + 64 c + lane, so x-neighbours across
+// chunks come from the adjacent chunk's registers and only the wave range's two edge
+// values per row are extra (wave-uniform) loads.
+template <int L>
+struct WIn {
+  static constexpr int XR = FCfg<L>::XR, CH = L / 4 / kWave;
+  double2 w[CH][XR + 2];
+  double el[XR + 2], er[XR + 2];
+};
+
+template <int L>
+__device__ __forceinline__ void load_w(WIn<L>& in, const double* __restrict__ w, int M, int s,
+                                       int wave, int lane) {
+  constexpr int XR = FCfg<L>::XR, CH = WIn<L>::CH, NX = 2 * L;
+  const int x0 = wave * (NX / 4);
+  const int xl = x0 == 0 ? NX - 1 : x0 - 1;
+  const int xr = x0 + NX / 4 == NX ? 0 : x0 + NX / 4;
+#pragma unroll
+  for (int j = 0; j < XR + 2; ++j) {
+    const double* row = w + (size_t)((s - 1 + j) & (M - 1)) * NX;
+    in.el[j] = row[xl];
+    in.er[j] = row[xr];
+#pragma unroll
+    for (int c = 0; c < CH; ++c)
+      in.w[c][j] = *reinterpret_cast<const double2*>(row + x0 + 2 * (c * kWave + lane));
+  }
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// The Win of chunk c, row j: x-1 / x+2 from the neighbouring lanes, across chunk edges
+// from the adjacent chunk (readlane), at the wave range's ends from the edge loads.
+template <int L>
+__device__ __forceinline__ Win w_win(const WIn<L>& in, int c, int j, int lane) {
+  constexpr int CH = WIn<L>::CH;
+  const double2 d = in.w[c][j];
+  Win o;
+  o.a = d.x;
+  o.b = d.y;
+  const double up = __shfl_up(d.y, 1, kWave);
+  const double dn = __shfl_down(d.x, 1, kWave);
+  const double lo = c == 0 ? in.el[j] : readlane_d(in.w[c > 0 ? c - 1 : 0][j].y, kWave - 1);
+  const double hi = c == CH - 1 ? in.er[j] : readlane_d(in.w[c < CH - 1 ? c + 1 : 0][j].x, 0);
+  o.l = lane == 0 ? lo : up;
+  o.r = lane == kWave - 1 ? hi : dn;
+  return o;
+}
+
 template <int L, int STAGE>
 __global__ __launch_bounds__(256) void vm_fused_stage_kernel(const FusedStageParams p) {
   using P = Plan<L>;
   using C = FCfg<L>;
   constexpr int XR = C::XR;
   constexpr int NX = 2 * L;
+  constexpr int CH = WIn<L>::CH;
   __shared__ double2 slots[C::NSLOT * C::SLOT];
   __shared__ TwLds<L> twL;
   __shared__ TwLds<2 * L> twN;
@@ -163,7 +218,7 @@ __global__ __launch_bounds__(256) void vm_fused_stage_kernel(const FusedStagePar
   const int g = threadIdx.x / P::T;  // row group of the transforms
   const int tid = threadIdx.x % P::T;
   const int lane = threadIdx.x & (kWave - 1);
-  const bool is_l = lane == 0, is_r = lane == kWave - 1;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x / kWave);
   const int s0 = xcd_remap(blockIdx.x, gridDim.x) * p.band;
   const int iters = p.band / XR;
   const StageCoef k = p.k;
@@ -171,17 +226,21 @@ __global__ __launch_bounds__(256) void vm_fused_stage_kernel(const FusedStagePar
   twL.fill(p.twL);
   twN.fill(p.twN);
   // priming: psi rows s0-1, s0 (slots 0, 1; rotated positions s0-2, s0-1), then
-  // s0+1 .. s0+XR (slots 2 .. XR+1; positions s0 .. s0+XR-1)
+  // s0+1 .. s0+XR (slots 2 .. XR+1; positions s0 .. s0+XR-1); the first stencil step's
+  // omega loads go out behind them
+  WIn<L> in;
   {
     HLoads<L> ld;
     load_h<L>(ld, p.HA, M, (s0 - 2) & (M - 1), 2);
+    HLoads<L> ld2;
+    load_h<L>(ld2, p.HA, M, s0, XR);
+    load_w<L>(in, p.w, M, s0, wave, lane);
     __syncthreads();  // twiddle tables
     pre_inv<L>(ld, slots, 0, 2, twN);
-    load_h<L>(ld, p.HA, M, s0, XR);
     __syncthreads();
     double2 v[16];
     run_stages_if<L, 0, 1, true>(slots + (g % C::NSLOT) * C::SLOT, v, tid, twL, g < 2);
-    pre_inv<L>(ld, slots, 2, XR, twN);
+    pre_inv<L>(ld2, slots, 2, XR, twN);
     __syncthreads();
     run_stages_if<L, 0, 1, true>(slots + ((2 + g) % C::NSLOT) * C::SLOT, v, tid, twL, true);
   }
@@ -192,45 +251,52 @@ __global__ __launch_bounds__(256) void vm_fused_stage_kernel(const FusedStagePar
     const bool more = it + 1 < iters;
 
     // ---- stencil rows s .. s+XR-1 -> HBM and registers --------------------------------
-    double2 res[C::CHUNKS][XR];
+    double2 wnv[CH][XR];
+    if constexpr (STAGE >= 2) {
 #pragma unroll
-    for (int c = 0; c < C::CHUNKS; ++c) {
-      const int pp = c * C::THREADS + threadIdx.x;  // x-pair: x = 2 pp
-      const int x = 2 * pp;
-      const int xl = x == 0 ? NX - 1 : x - 1;
-      const int xr = x + 2 >= NX ? x + 2 - NX : x + 2;
+      for (int j = 0; j < XR; ++j)
+#pragma unroll
+        for (int c = 0; c < CH; ++c)
+          wnv[c][j] = *reinterpret_cast<const double2*>(
+              p.wn + (size_t)(s + j) * NX + wave * (NX / 4) + 2 * (c * kWave + lane));
+    }
+    double2 res[CH][XR];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) {
+      const int pp = wave * (L / 4) + c * kWave + lane;  // x-pair: x = 2 pp
       Win w[XR + 2], sv[XR + 2];
 #pragma unroll
       for (int j = 0; j < XR + 2; ++j) {
-        const int y = (s - 1 + j) & (M - 1);
-        w[j] = expand(fetch(p.w + (size_t)y * NX, x, xl, xr, is_l, is_r), is_l, is_r);
+        w[j] = w_win<L>(in, c, j, lane);
         sv[j] = psi_win<L>(slots + ((sf + j) % C::NSLOT) * C::SLOT, pp);
       }
 #pragma unroll
       for (int j = 0; j < XR; ++j) {
-        const size_t o = (size_t)(s + j) * NX + x;
-        double2 wnv = make_double2(0.0, 0.0);
-        if constexpr (STAGE >= 2) wnv = *reinterpret_cast<const double2*>(p.wn + o);
         double r0, r1;
         pair_rhs(w[j], w[j + 1], w[j + 2], sv[j], sv[j + 1], sv[j + 2], k, r0, r1);
+        const double2 wv = STAGE >= 2 ? wnv[c][j] : make_double2(0.0, 0.0);
         double2 out;
-        out.x = stage_update<STAGE>(r0, w[j + 1].a, wnv.x, k);
-        out.y = stage_update<STAGE>(r1, w[j + 1].b, wnv.y, k);
-        *reinterpret_cast<double2*>(p.out + o) = out;
+        out.x = stage_update<STAGE>(r0, w[j + 1].a, wv.x, k);
+        out.y = stage_update<STAGE>(r1, w[j + 1].b, wv.y, k);
+        *reinterpret_cast<double2*>(p.out + (size_t)(s + j) * NX + 2 * pp) = out;
         res[c][j] = out;
       }
     }
-    // prefetch the next psi rows' spectrum (consumed after the forward transform)
+    // prefetch: the next psi rows' spectrum and the next step's omega rows (consumed after
+    // the transforms)
     HLoads<L> ld;
-    if (more) load_h<L>(ld, p.HA, M, s + XR, XR);
+    if (more) {
+      load_h<L>(ld, p.HA, M, s + XR, XR);
+      load_w<L>(in, p.w, M, s + XR, wave, lane);
+    }
     __syncthreads();  // every psi read of the dead slots is done
 
     // ---- output rows -> next stage's spectrum -----------------------------------------
     double2 v[16];
     if (p.write_spec) {
 #pragma unroll
-      for (int c = 0; c < C::CHUNKS; ++c) {
-        const int pp = c * C::THREADS + threadIdx.x;
+      for (int c = 0; c < CH; ++c) {
+        const int pp = wave * (L / 4) + c * kWave + lane;
 #pragma unroll
         for (int j = 0; j < XR; ++j) slots[((sf + j) % C::NSLOT) * C::SLOT + padx(pp)] = res[c][j];
       }
