@@ -161,7 +161,9 @@ struct WIn {
   double el[XR + 2], er[XR + 2];
 };
 
-template <int L>
+// Rows s-1+j, j = J0 .. XR+1, of a stencil step (J0 = 2: the step's first two rows are the
+// previous step's last two, carried by shift_w).
+template <int L, int J0 = 0>
 __device__ __forceinline__ void load_w(WIn<L>& in, const double* __restrict__ w, int M, int s,
                                        int wave, int lane) {
   constexpr int XR = FCfg<L>::XR, CH = WIn<L>::CH, NX = 2 * L;
@@ -169,7 +171,7 @@ __device__ __forceinline__ void load_w(WIn<L>& in, const double* __restrict__ w,
   const int xl = x0 == 0 ? NX - 1 : x0 - 1;
   const int xr = x0 + NX / 4 == NX ? 0 : x0 + NX / 4;
 #pragma unroll
-  for (int j = 0; j < XR + 2; ++j) {
+  for (int j = J0; j < XR + 2; ++j) {
     const double* row = w + (size_t)((s - 1 + j) & (M - 1)) * NX;
     in.el[j] = row[xl];
     in.er[j] = row[xr];
@@ -184,6 +186,19 @@ __device__ __forceinline__ double readlane_d(double v, int l) {
   const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)b, l);
   const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+// Rows s+XR-1, s+XR of a step are rows s'-1, s' of the next (s' = s + XR): keep them.
+template <int L>
+__device__ __forceinline__ void shift_w(WIn<L>& in) {
+  constexpr int XR = FCfg<L>::XR, CH = WIn<L>::CH;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    in.el[j] = in.el[XR + j];
+    in.er[j] = in.er[XR + j];
+#pragma unroll
+    for (int c = 0; c < CH; ++c) in.w[c][j] = in.w[c][XR + j];
+  }
 }
 
 // The Win of chunk c, row j: x-1 / x+2 from the neighbouring lanes, across chunk edges
@@ -287,7 +302,8 @@ __global__ __launch_bounds__(256) void vm_fused_stage_kernel(const FusedStagePar
     HLoads<L> ld;
     if (more) {
       load_h<L>(ld, p.HA, M, s + XR, XR);
-      load_w<L>(in, p.w, M, s + XR, wave, lane);
+      shift_w<L>(in);
+      load_w<L, 2>(in, p.w, M, s + XR, wave, lane);
     }
     __syncthreads();  // every psi read of the dead slots is done
 

@@ -73,7 +73,15 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
     double2 o;
     o.x = stage_update<STAGE>(r0, wc.a, wnv.x, k);
     o.y = stage_update<STAGE>(r1, wc.b, wnv.y, k);
+#ifdef CFDJ_NT_OUT
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    if (valid) {
+      d2v ov = {o.x, o.y};
+      __builtin_nontemporal_store(ov, reinterpret_cast<d2v*>(p.out + (size_t)y * nx + xs));
+    }
+#else
     if (valid) *reinterpret_cast<double2*>(p.out + (size_t)y * nx + xs) = o;
+#endif
 
     wm = wc;
     wc = wp;

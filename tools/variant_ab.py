@@ -1,4 +1,4 @@
-"""Per-launch time of the FFT-fused stage kernels (cfdj_vm_kernel_bench ids 7-10) for each
+"""Per-launch time of step kernels (cfdj_vm_kernel_bench ids in $KB_IDS, default 1-6) for each
 libcfdj variant given on the command line (built by tools/build_variant.sh); one process
 per variant.  python tools/fstage_ab.py build/a/libcfdj.so build/b/libcfdj.so ..."""
 import json, os, subprocess, sys
@@ -14,7 +14,7 @@ h = VortexMerger(n, n, dx, dx, 1000.0, device=0)
 x = dx * np.arange(n + 1)
 wn = np.zeros((n + 2, n + 2), order="F"); vm_ic(n, n, x, x, wn); h.upload(wn)
 h.step(5e-4, 1)
-print(json.dumps({k: round(h.kernel_bench(k, 5e-4, 20) * 1e3, 1) for k in (1, 7, 8, 9, 10)}))
+print(json.dumps({k: round(h.kernel_bench(k, 5e-4, 20) * 1e3, 1) for k in [int(i) for i in os.environ.get("KB_IDS", "1,2,3,4,5,6").split(",")]}))
 '''
 for lib in sys.argv[1:]:
     env = dict(os.environ, CFDJ_LIB=lib)
