@@ -29,6 +29,7 @@ KB_NAMES = {1: "vm_stage_kernel<1>", 2: "vm_stage_kernel<2>", 3: "vm_stage_kerne
 POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED, POISSON_SCHUR = 0, 1, 2, 3
 SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1
 CAVITY_DST, CAVITY_MG = 0, 1
+SPEC_HYBRID, SPEC_PS23, SPEC_PS32 = 0, 1, 2
 
 
 class CfdjError(RuntimeError):
@@ -109,6 +110,15 @@ SIGNATURES = {
     "cfdj_jacobi_solve": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, _dp, C.c_long,
                                     _dp, C.c_long, C.c_long, C.c_double, C.c_long, _lp, _dp]),
     "cfdj_ftcs": (C.c_int, [C.c_int, C.c_int, C.c_double, _dp, _dp, C.c_long]),
+    "cfdj_spec_create": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double,
+                                   C.c_double, C.c_int, C.c_int, C.POINTER(_vp)]),
+    "cfdj_spec_upload": (C.c_int, [_vp, _dp, C.c_long]),
+    "cfdj_spec_step": (C.c_int, [_vp, C.c_double, C.c_int]),
+    "cfdj_spec_download": (C.c_int, [_vp, _dp, C.c_long]),
+    "cfdj_spec_get_spectrum": (C.c_int, [_vp, _dp]),
+    "cfdj_spec_set_spectrum": (C.c_int, [_vp, _dp]),
+    "cfdj_spec_jacobian": (C.c_int, [_vp, _dp, _dp]),
+    "cfdj_spec_destroy": (None, [_vp]),
 }
 
 _lock = threading.Lock()

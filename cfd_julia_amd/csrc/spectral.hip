@@ -1,0 +1,458 @@
+// Spectral-space NS2D solvers of the reference:
+//   20_NS2D_Hybrid_Solver/hybrid.jl                         (CFDJ_SPEC_HYBRID)
+//   22_NS2D_PseudoSpectral_23_Rule/pseudospectral_23_rule.jl (CFDJ_SPEC_PS23)
+//   21_NS2D_PseudoSpectral_32_Rule/pseudospectral_32_rule.jl (CFDJ_SPEC_PS32)
+//
+// All three advance the full complex vorticity spectrum w_f (nx x ny, column-major like
+// the reference's Array{ComplexF64}) with the same low-storage RK3 / Crank-Nicolson loop
+// (hybrid.jl:41-67) and differ in the Jacobian jf = fft(-J(w, psi)).  The reference never
+// assumes Hermitian symmetry (kx[1] = eps and its Nyquist derivatives are not odd), so the
+// transforms here are rocFFT complex-to-complex, with real(ifft(.)) taken as written.
+//
+// Per Jacobian evaluation (one RK3 substep):
+//   hybrid: [w_f, w_f / k2] -> batch-2 inverse c2c -> Arakawa stencil on the real parts
+//           (hybrid.jl:129-150, per-term gg) -> forward c2c;
+//   2/3:    psi_x, w_y, psi_y, w_x spectra with the 2/3-rule modes zeroed -> batch-4
+//           inverse c2c -> psi_x w_y - psi_y w_x -> forward c2c;
+//   3/2:    the same four spectra zero-padded to (3nx/2) x (3ny/2) by quadrant copies,
+//           scaled by (nxe nye)/(nx ny) -> batch-4 inverse c2c -> product -> forward c2c
+//           -> quadrants back, scaled by (nx ny)/(nxe nye).
+// Elementwise arithmetic follows the source order (Julia Real*Complex and Complex/Real
+// act componentwise), built with -ffp-contract=off like the rest of the library.
+#include <cmath>
+#include <memory>
+
+#include "host_common.hpp"
+
+namespace cfdj {
+
+namespace {
+
+struct SpecDims {
+  int nx, ny;        // spectral grid
+  int px, py;        // transform grid of the products (padded for the 3/2 rule)
+  double inv_n;      // 1 / (nx ny)      (real(ifft) scale on the nx x ny grid)
+  double inv_np;     // 1 / (px py)
+};
+
+__device__ __forceinline__ double2 cmul_r(double a, double2 e) { return make_double2(a * e.x, a * e.y); }
+__device__ __forceinline__ double2 cdiv_r(double2 e, double d) { return make_double2(e.x / d, e.y / d); }
+__device__ __forceinline__ double2 times_i(double2 e) { return make_double2(-e.y, e.x); }
+
+// complex(w, 0) of a pitched real nx x ny block (hybrid.jl:24).
+__global__ void to_complex_kernel(const double* __restrict__ w, long ldw, double2* __restrict__ out,
+                                  int nx, int ny) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    out[t] = make_double2(w[(size_t)j * ldw + i], 0.0);
+  }
+}
+
+// hybrid.jl:103,115: X0 = w_f (for w), X1 = w_f / k2 (for psi).
+__global__ void hybrid_prep_kernel(const double2* __restrict__ wf, const double* __restrict__ kx,
+                                   double2* __restrict__ X, int nx, int ny) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const double k2 = kx[i] * kx[i] + kx[j] * kx[j];
+    const double2 v = wf[t];
+    X[t] = v;
+    X[n + t] = cdiv_r(v, k2);
+  }
+}
+
+// hybrid.jl:129-150 on the periodic grid: data = complex(-(j1 + j2 + j3) * hh, 0) with
+// w = Re(X0) / N, s = Re(X1) / N (real(ifft)).
+__global__ void hybrid_jac_kernel(const double2* __restrict__ X, double2* __restrict__ J, int nx,
+                                  int ny, double inv_n, double gg, double hh) {
+  const size_t n = (size_t)nx * ny;
+  const double2* S = X + n;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const int ie = i + 1 == nx ? 0 : i + 1, iw = i == 0 ? nx - 1 : i - 1;
+    const int jn = j + 1 == ny ? 0 : j + 1, js = j == 0 ? ny - 1 : j - 1;
+    auto W = [&](int a, int b) { return X[(size_t)b * nx + a].x * inv_n; };
+    auto P = [&](int a, int b) { return S[(size_t)b * nx + a].x * inv_n; };
+    const double wE = W(ie, j), wW = W(iw, j), wN = W(i, jn), wS = W(i, js);
+    const double wNE = W(ie, jn), wSW = W(iw, js), wNW = W(iw, jn), wSE = W(ie, js);
+    const double sE = P(ie, j), sW = P(iw, j), sN = P(i, jn), sS = P(i, js);
+    const double sNE = P(ie, jn), sSW = P(iw, js), sNW = P(iw, jn), sSE = P(ie, js);
+    const double j1 = gg * ((wE - wW) * (sN - sS) - (wN - wS) * (sE - sW));
+    const double j2 =
+        gg * (wE * (sNE - sSE) - wW * (sNW - sSW) - wN * (sNE - sNW) + wS * (sSE - sSW));
+    const double j3 =
+        gg * (wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS));
+    J[t] = make_double2(-(j1 + j2 + j3) * hh, 0.0);
+  }
+}
+
+// pseudospectral_*.jl:109-122 derivatives of w_f, placed on the px x py product grid:
+//   2/3 rule (px = nx): modes i in [nxe/2, nx - nxe/2) or j in [nye/2, ny - nye/2) zeroed
+//           (pseudospectral_23_rule.jl:124-133, 0-based);
+//   3/2 rule (px = 3nx/2): quadrant copies (pseudospectral_32_rule.jl:124-154), everything
+//           else zero, times (nxe nye) then divided by (nx ny).
+// One thread per element of the px x py grid; batch b of D is j_{b+1} f.
+__global__ void ps_derivs_kernel(const double2* __restrict__ wf, const double* __restrict__ kx,
+                                 double2* __restrict__ D, int nx, int ny, int px, int py,
+                                 int rule32, int tx0, int tx1, int ty0, int ty1, double sc,
+                                 double sd) {
+  const size_t np = (size_t)px * py;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < np;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int a = (int)(t % px), b = (int)(t / px);
+    int i = a, j = b;
+    bool keep;
+    if (rule32) {
+      const int hx = nx / 2, hy = ny / 2, qx = px - hx, qy = py - hy;
+      keep = (a < hx || a >= qx) && (b < hy || b >= qy);
+      i = a < hx ? a : a - qx + hx;
+      j = b < hy ? b : b - qy + hy;
+    } else {
+      keep = !(a >= tx0 && a < tx1) && !(b >= ty0 && b < ty1);
+    }
+    double2 d1 = make_double2(0.0, 0.0), d2 = d1, d3 = d1, d4 = d1;
+    if (keep) {
+      const double kxi = kx[i], kyj = kx[j];
+      const double k2 = kxi * kxi + kyj * kyj;
+      const double2 iw = times_i(wf[(size_t)j * nx + i]);
+      d1 = cdiv_r(cmul_r(kxi, iw), k2);  // 1im * wf * kx / k2
+      d4 = cmul_r(kxi, iw);              // 1im * wf * kx
+      d2 = cmul_r(kyj, iw);              // 1im * wf * ky
+      d3 = cdiv_r(cmul_r(kyj, iw), k2);  // 1im * wf * ky / k2
+      if (rule32) {
+        d1 = make_double2(d1.x * sc / sd, d1.y * sc / sd);
+        d2 = make_double2(d2.x * sc / sd, d2.y * sc / sd);
+        d3 = make_double2(d3.x * sc / sd, d3.y * sc / sd);
+        d4 = make_double2(d4.x * sc / sd, d4.y * sc / sd);
+      }
+    }
+    D[t] = d1;
+    D[np + t] = d2;
+    D[2 * np + t] = d3;
+    D[3 * np + t] = d4;
+  }
+}
+
+// jacp = j1 j2 - j3 j4 with j_k = real(ifft(.)) = Re(D_k) / (px py).
+__global__ void ps_product_kernel(const double2* __restrict__ D, double2* __restrict__ J, size_t np,
+                                  double inv_np) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < np;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const double j1 = D[t].x * inv_np, j2 = D[np + t].x * inv_np;
+    const double j3 = D[2 * np + t].x * inv_np, j4 = D[3 * np + t].x * inv_np;
+    J[t] = make_double2(j1 * j2 - j3 * j4, 0.0);
+  }
+}
+
+// pseudospectral_32_rule.jl:171-178: quadrants of the padded product spectrum, * (nx ny)
+// / (nxe nye).
+__global__ void ps_unpad_kernel(const double2* __restrict__ Jp, double2* __restrict__ jf, int nx,
+                                int ny, int px, int py, double sd, double sc) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const int hx = nx / 2, hy = ny / 2;
+    const int a = i < hx ? i : i - hx + (px - hx), b = j < hy ? j : j - hy + (py - hy);
+    const double2 v = Jp[(size_t)b * px + a];
+    jf[t] = make_double2(v.x * sd / sc, v.y * sd / sc);
+  }
+}
+
+// hybrid.jl:44-67, one RK3 / Crank-Nicolson substep.  z = .5dt k2 / re, d = alpha z;
+// out = ((1 - d)/(1 + d)) * w + (cA * jA + cB * jB) / (1 + d)   (stage 1: cB = 0, no jB);
+// out[1,1] = 0 after stages 1 and 2.
+template <int STAGE>
+__global__ void cn_update_kernel(const double2* __restrict__ w, const double2* __restrict__ jA,
+                                 const double2* __restrict__ jB, double2* __restrict__ out,
+                                 const double* __restrict__ kx, int nx, int ny, double hdt,
+                                 double re, double alpha, double cA, double cB) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const double k2 = kx[i] * kx[i] + kx[j] * kx[j];
+    const double z = hdt * k2 / re;
+    const double d = alpha * z;
+    const double g = (1.0 - d) / (1.0 + d);
+    const double e = 1.0 + d;
+    const double2 wv = w[t];
+    double2 f = cmul_r(cA, jA[t]);
+    if constexpr (STAGE >= 2) {
+      const double2 fb = cmul_r(cB, jB[t]);
+      f = make_double2(f.x + fb.x, f.y + fb.y);
+    }
+    double2 o = make_double2(g * wv.x + f.x / e, g * wv.y + f.y / e);
+    if (STAGE <= 2 && t == 0) o = make_double2(0.0, 0.0);
+    out[t] = o;
+  }
+}
+
+// hybrid.jl:71-76: ut[1:nx,1:ny] = real(ifft(w_f)), ut[nx+1,:] = ut[1,:], ut[:,ny+1] = ut[:,1];
+// written into a pitched (nx+1) x (ny+1) block.
+__global__ void to_field_kernel(const double2* __restrict__ X, double* __restrict__ ut, long ldu,
+                                int nx, int ny, double inv_n) {
+  const size_t n = (size_t)(nx + 1) * (ny + 1);
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % (nx + 1)), j = (int)(t / (nx + 1));
+    const int a = i == nx ? 0 : i, b = j == ny ? 0 : j;
+    ut[(size_t)j * ldu + i] = X[(size_t)b * nx + a].x * inv_n;
+  }
+}
+
+unsigned grid_for(size_t n) {
+  size_t b = (n + 255) / 256;
+  if (b > 65536) b = 65536;
+  return (unsigned)(b ? b : 1);
+}
+
+}  // namespace
+
+}  // namespace cfdj
+
+using namespace cfdj;
+
+struct cfdj_spec {
+  int kind = CFDJ_SPEC_HYBRID;
+  int nx = 0, ny = 0, px = 0, py = 0;
+  double dx = 0, dy = 0, re = 0, eps = 0;
+  int device = -1;
+  hipStream_t stream = nullptr;
+  double* kx = nullptr;
+  double2 *wn = nullptr, *w1 = nullptr, *w2 = nullptr;   // spectra of the RK3 loop
+  double2 *jn = nullptr, *j1 = nullptr, *j2 = nullptr;   // Jacobians
+  double2* X = nullptr;   // hybrid: [w_f, w_f/k2]; PS: 4 derivative spectra (px x py)
+  double2* J = nullptr;   // product grid (px x py): physical product -> its spectrum
+  double* field = nullptr;  // (nx+1) x (ny+1) download staging
+  Plans plans;
+  rocfft_plan fwd = nullptr, inv = nullptr;      // nx x ny, batch 1 (in place)
+  rocfft_plan inv_b = nullptr, fwd_p = nullptr;  // product grid: batch 2 / 4 inverse, forward
+
+  size_t n() const { return (size_t)nx * ny; }
+  size_t np() const { return (size_t)px * py; }
+
+  // jf = fft(-J(w, psi)) of the spectrum wf (hybrid.jl:92-152 / pseudospectral_*.jl).
+  void jacobian(const double2* wf, double2* jf) {
+    const unsigned gb = grid_for(np());
+    if (kind == CFDJ_SPEC_HYBRID) {
+      hipLaunchKernelGGL(hybrid_prep_kernel, dim3(grid_for(n())), dim3(256), 0, stream, wf, kx,
+                         X, nx, ny);
+      CFDJ_HIP(hipGetLastError());
+      plans.exec(inv_b, X, nullptr);
+      const double gg = 1.0 / (4.0 * dx * dy), hh = 1.0 / 3.0;
+      hipLaunchKernelGGL(hybrid_jac_kernel, dim3(grid_for(n())), dim3(256), 0, stream, X, jf,
+                         nx, ny, 1.0 / ((double)nx * ny), gg, hh);
+      CFDJ_HIP(hipGetLastError());
+      plans.exec(fwd, jf, nullptr);
+      return;
+    }
+    const bool r32 = kind == CFDJ_SPEC_PS32;
+    const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
+    const int tx0 = nxe / 2, tx1 = nx - nxe / 2, ty0 = nye / 2, ty1 = ny - nye / 2;
+    const double sc = (double)px * py, sd = (double)nx * ny;
+    hipLaunchKernelGGL(ps_derivs_kernel, dim3(gb), dim3(256), 0, stream, wf, kx, X, nx, ny, px,
+                       py, r32 ? 1 : 0, tx0, tx1, ty0, ty1, sc, sd);
+    CFDJ_HIP(hipGetLastError());
+    plans.exec(inv_b, X, nullptr);
+    double2* P = r32 ? J : jf;
+    hipLaunchKernelGGL(ps_product_kernel, dim3(gb), dim3(256), 0, stream, X, P, np(),
+                       1.0 / sc);
+    CFDJ_HIP(hipGetLastError());
+    plans.exec(r32 ? fwd_p : fwd, P, nullptr);
+    if (r32) {
+      hipLaunchKernelGGL(ps_unpad_kernel, dim3(grid_for(n())), dim3(256), 0, stream, J, jf, nx,
+                         ny, px, py, sd, sc);
+      CFDJ_HIP(hipGetLastError());
+    }
+  }
+
+  template <int STAGE>
+  void update(const double2* w, const double2* jA, const double2* jB, double2* out, double dt,
+              double alpha, double cA, double cB) {
+    hipLaunchKernelGGL(cn_update_kernel<STAGE>, dim3(grid_for(n())), dim3(256), 0, stream, w,
+                       jA, jB, out, kx, nx, ny, 0.5 * dt, re, alpha, cA, cB);
+    CFDJ_HIP(hipGetLastError());
+  }
+
+  // hybrid.jl:41-67 (alpha, gamma, rho of hybrid.jl:30-32)
+  void step(double dt) {
+    const double a1 = 8.0 / 15.0, a2 = 2.0 / 15.0, a3 = 1.0 / 3.0;
+    const double g1 = 8.0 / 15.0, g2 = 5.0 / 12.0, g3 = 3.0 / 4.0;
+    const double r2 = -17.0 / 60.0, r3 = -5.0 / 12.0;
+    jacobian(wn, jn);
+    update<1>(wn, jn, nullptr, w1, dt, a1, g1 * dt, 0.0);
+    jacobian(w1, j1);
+    update<2>(w1, jn, j1, w2, dt, a2, r2 * dt, g2 * dt);
+    jacobian(w2, j2);
+    update<3>(w2, j1, j2, wn, dt, a3, r3 * dt, g3 * dt);
+  }
+
+  ~cfdj_spec() {
+    if (stream) (void)hipStreamSynchronize(stream);
+    plans.destroy();
+    for (double2** p : {&wn, &w1, &w2, &jn, &j1, &j2, &X, &J}) dfree(*p);
+    dfree(kx);
+    dfree(field);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+};
+
+extern "C" {
+
+int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps, int kind,
+                     int device, cfdj_spec** out) {
+  return guard([&] {
+    CFDJ_REQUIRE(out != nullptr, "out is NULL");
+    *out = nullptr;
+    CFDJ_REQUIRE(kind == CFDJ_SPEC_HYBRID || kind == CFDJ_SPEC_PS23 || kind == CFDJ_SPEC_PS32,
+                 "bad solver kind");
+    CFDJ_REQUIRE(nx == ny, "the spectral solvers alias ky = kx (Common.jl:198): nx == ny");
+    CFDJ_REQUIRE(nx >= 8 && nx % 2 == 0, "nx must be even and >= 8 (kx loops to nx/2)");
+    CFDJ_REQUIRE(dx > 0 && dy > 0 && std::isfinite(re) && re != 0.0, "bad dx, dy or re");
+    fft_setup();
+    select_device(device);
+    std::unique_ptr<cfdj_spec> h(new cfdj_spec);
+    CFDJ_HIP(hipGetDevice(&h->device));
+    CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
+    h->kind = kind;
+    h->nx = nx;
+    h->ny = ny;
+    h->dx = dx;
+    h->dy = dy;
+    h->re = re;
+    h->eps = eps;
+    h->px = kind == CFDJ_SPEC_PS32 ? (3 * nx) / 2 : nx;
+    h->py = kind == CFDJ_SPEC_PS32 ? (3 * ny) / 2 : ny;
+    // Common.jl:190-196: hx = 2pi / (nx dx); kx[i] = hx (i-1), kx[i+nx/2] = hx (i-nx/2-1)
+    std::vector<double> k(nx);
+    const double hx = (2.0 * M_PI) / ((double)nx * dx);
+    for (int i = 1; i <= nx / 2; ++i) {
+      k[i - 1] = hx * (i - 1.0);
+      k[i + nx / 2 - 1] = hx * (double)(i - nx / 2 - 1);
+    }
+    k[0] = eps;
+    h->kx = dalloc<double>(nx);
+    CFDJ_HIP(hipMemcpy(h->kx, k.data(), nx * sizeof(double), hipMemcpyHostToDevice));
+    const size_t n = h->n(), np = h->np();
+    for (double2** p : {&h->wn, &h->w1, &h->w2, &h->jn, &h->j1, &h->j2}) {
+      *p = dalloc<double2>(n);
+      CFDJ_HIP(hipMemset(*p, 0, n * sizeof(double2)));
+    }
+    const int nb = kind == CFDJ_SPEC_HYBRID ? 2 : 4;
+    h->X = dalloc<double2>((size_t)nb * np);
+    if (kind == CFDJ_SPEC_PS32) h->J = dalloc<double2>(np);
+    h->field = dalloc<double>((size_t)(nx + 1) * (ny + 1));
+    size_t lens[2] = {(size_t)nx, (size_t)ny};
+    size_t lp[2] = {(size_t)h->px, (size_t)h->py};
+    h->fwd = h->plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 2,
+                          lens, 1, nullptr);
+    h->inv = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
+                          lens, 1, nullptr);
+    h->inv_b = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
+                            lp, nb, nullptr);
+    if (kind == CFDJ_SPEC_PS32)
+      h->fwd_p = h->plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace,
+                              2, lp, 1, nullptr);
+    h->plans.finalize(h->stream);
+    *out = h.release();
+  });
+}
+
+// hybrid.jl:24-28: w_f = fft(complex(wn[2:nx+1, 2:ny+1])); w_f[1,1] = 0.
+int cfdj_spec_upload(cfdj_spec* h, const double* wn, long ldw) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && wn, "NULL argument");
+    CFDJ_REQUIRE(ldw >= (long)h->nx + 2, "ldw: leading dimension too small");
+    select_device(h->device);
+    const int nx = h->nx, ny = h->ny;
+    CFDJ_HIP(hipMemcpy2DAsync(h->field, (nx + 1) * sizeof(double), wn + 1 + ldw,
+                              ldw * sizeof(double), nx * sizeof(double), ny,
+                              hipMemcpyHostToDevice, h->stream));
+    hipLaunchKernelGGL(to_complex_kernel, dim3(grid_for(h->n())), dim3(256), 0, h->stream,
+                       h->field, (long)(nx + 1), h->wn, nx, ny);
+    CFDJ_HIP(hipGetLastError());
+    h->plans.exec(h->fwd, h->wn, nullptr);
+    CFDJ_HIP(hipMemsetAsync(h->wn, 0, sizeof(double2), h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_spec_step(cfdj_spec* h, double dt, int nsteps) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    CFDJ_REQUIRE(nsteps >= 0 && std::isfinite(dt), "bad dt or nsteps");
+    select_device(h->device);
+    for (int k = 0; k < nsteps; ++k) h->step(dt);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+// hybrid.jl:71-76: ut = real(ifft(w_f)) with the periodic row / column, (nx+1) x (ny+1).
+int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && ut, "NULL argument");
+    CFDJ_REQUIRE(ldu >= (long)h->nx + 1, "ldu: leading dimension too small");
+    select_device(h->device);
+    const int nx = h->nx, ny = h->ny;
+    CFDJ_HIP(hipMemcpyAsync(h->j2, h->wn, h->n() * sizeof(double2), hipMemcpyDeviceToDevice,
+                            h->stream));  // j2 is scratch between steps
+    h->plans.exec(h->inv, h->j2, nullptr);
+    hipLaunchKernelGGL(to_field_kernel, dim3(grid_for((size_t)(nx + 1) * (ny + 1))), dim3(256),
+                       0, h->stream, h->j2, h->field, (long)(nx + 1), nx, ny,
+                       1.0 / ((double)nx * ny));
+    CFDJ_HIP(hipGetLastError());
+    CFDJ_HIP(hipMemcpy2DAsync(ut, ldu * sizeof(double), h->field, (nx + 1) * sizeof(double),
+                              (nx + 1) * sizeof(double), ny + 1, hipMemcpyDeviceToHost,
+                              h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+// The spectrum itself (complex nx x ny, column-major, interleaved re/im), in and out.
+int cfdj_spec_get_spectrum(cfdj_spec* h, double* wf) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && wf, "NULL argument");
+    select_device(h->device);
+    CFDJ_HIP(hipMemcpyAsync(wf, h->wn, h->n() * sizeof(double2), hipMemcpyDeviceToHost,
+                            h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+int cfdj_spec_set_spectrum(cfdj_spec* h, const double* wf) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && wf, "NULL argument");
+    select_device(h->device);
+    CFDJ_HIP(hipMemcpyAsync(h->wn, wf, h->n() * sizeof(double2), hipMemcpyHostToDevice,
+                            h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+// One Jacobian evaluation jf = fft(-J(w, psi)) of the spectrum wf (both complex nx x ny).
+int cfdj_spec_jacobian(cfdj_spec* h, const double* wf, double* jf) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && wf && jf, "NULL argument");
+    select_device(h->device);
+    const size_t b = h->n() * sizeof(double2);
+    CFDJ_HIP(hipMemcpyAsync(h->w2, wf, b, hipMemcpyHostToDevice, h->stream));
+    h->jacobian(h->w2, h->j2);
+    CFDJ_HIP(hipMemcpyAsync(jf, h->j2, b, hipMemcpyDeviceToHost, h->stream));
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
+void cfdj_spec_destroy(cfdj_spec* h) {
+  if (!h) return;
+  (void)guard([&] {
+    select_device(h->device);
+    delete h;
+  });
+}
+
+}  // extern "C"

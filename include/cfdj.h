@@ -223,6 +223,32 @@ int cfdj_jacobi_solve(int nx, int ny, double dx, double dy, const double* f, lon
                       double* u, long ldu, long max_iter, double tol, long freq,
                       long* iterations, double* rms);
 
+/* ---- spectral NS2D: 20_NS2D_Hybrid_Solver/hybrid.jl, 21/22 pseudospectral -------------
+ * The vorticity spectrum w_f (complex nx x ny, as the reference's Array{ComplexF64}) is
+ * advanced by the low-storage RK3 / Crank-Nicolson loop of hybrid.jl:41-67 (identical in
+ * pseudospectral_32_rule.jl and pseudospectral_23_rule.jl); `kind` selects `jacobian`:
+ * hybrid.jl:92-152 (Arakawa in physical space), pseudospectral_23_rule.jl:95-144 (2/3-rule
+ * truncation) or pseudospectral_32_rule.jl:94-186 (3/2-rule padding).  Square even grids
+ * (the reference aliases ky = kx, Common.jl:198). */
+typedef struct cfdj_spec cfdj_spec;
+#define CFDJ_SPEC_HYBRID 0
+#define CFDJ_SPEC_PS23 1
+#define CFDJ_SPEC_PS32 2
+int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps, int kind,
+                     int device, cfdj_spec** out);
+/* hybrid.jl:24-28: w_f = fft(wn[2:nx+1, 2:ny+1]), w_f[1,1] = 0 (wn ghosted, ld >= nx+2). */
+int cfdj_spec_upload(cfdj_spec* h, const double* wn, long ldw);
+/* nsteps iterations of hybrid.jl:41-67. */
+int cfdj_spec_step(cfdj_spec* h, double dt, int nsteps);
+/* hybrid.jl:71-76: ut = real(ifft(w_f)) on (nx+1) x (ny+1) nodes (ld >= nx+1). */
+int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu);
+/* w_f itself, complex nx x ny column-major as interleaved (re, im) doubles. */
+int cfdj_spec_get_spectrum(cfdj_spec* h, double* wf);
+int cfdj_spec_set_spectrum(cfdj_spec* h, const double* wf);
+/* One `jacobian(nx, ny, dx, dy, wf, k2)` call: jf = fft(-J(w, psi)) (complex, as above). */
+int cfdj_spec_jacobian(cfdj_spec* h, const double* wf, double* jf);
+void cfdj_spec_destroy(cfdj_spec* h);
+
 /* ---- 01_Heat_Equation_FTCS/ftcs.jl:34-41 (host code: BASELINE config 1 is CPU-only) -------
  * un is (nx+1) x (nt+1) column-major (ld >= nx+1): column 0 is u0, column k the FTCS step
  * u_i <- u_i + beta (u_{i+1} - 2 u_i + u_{i-1}) with u_0 = u_nx = 0. */

@@ -1,0 +1,92 @@
+"""GPU parity of the spectral-space NS2D solvers (libcfdj.so `cfdj_spec_*`, spectral.hip)
+against oracle/spectral_oracle.py -- the CPU restatement of
+20_NS2D_Hybrid_Solver/hybrid.jl and the 2/3- and 3/2-rule pseudospectral scripts.
+
+Tolerances: one Jacobian evaluation 1e-12 relative to max|jf| (FFT round-off: rocFFT vs
+pocketfft); vorticity after K steps L-inf < 1e-10 (north-star bound, |w| ~ 1); the
+Taylor-Green known answer (zero Jacobian, exact scheme decay) to 1e-12.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from oracle import spectral_oracle as so
+from oracle import vm_oracle as vo
+from tests.golden.make_golden import smooth_field
+
+pytestmark = pytest.mark.gpu
+KINDS = ["hybrid", "2/3", "3/2"]
+KIND_ID = {"hybrid": so.HYBRID, "2/3": so.PS23, "3/2": so.PS32}
+
+
+@pytest.fixture(scope="module")
+def spec():
+    from cfd_julia_amd import _lib, spectral
+
+    assert _lib.require_gpu() >= 1
+    return spectral
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("n", [64, 96, 256])
+def test_gpu_spectral_jacobian_vs_oracle(spec, kind, n):
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    f = smooth_field(n, n, 6, n) + 0.01 * np.random.default_rng(n).standard_normal((n, n))
+    wf = so.to_spectral(f)
+    k2 = so.wavespace(n, n, dx, dy)
+    ref = so.JACOBIANS[KIND_ID[kind]](wf, k2, dx, dy)
+    with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+        got = h.jacobian(wf)
+    assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("n,steps,dt", [(128, 20, 0.01), (256, 10, 0.005)])
+def test_gpu_spectral_vm_steps_vs_oracle(spec, kind, n, steps, dt):
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    ref = so.numerical(w0, steps, dt, dx, dy, 1000.0, KIND_ID[kind])
+    with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+        h.upload_interior(w0)
+        h.step(dt, steps)
+        ut = h.download()
+        wf = h.spectrum()
+    assert np.abs(ut[:n, :n] - ref).max() < 1e-10
+    assert np.array_equal(ut[n, :], ut[0, :]) and np.array_equal(ut[:, n], ut[:, 0])
+    assert wf[0, 0] == 0 or abs(wf[0, 0]) < 1e-9  # hybrid.jl:59 zeroes stages 1-2 only
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_gpu_spectral_tgv_known_answer(spec, kind):
+    """Taylor-Green: J(w, psi) = 0, so the field decays by the scheme's exact factor."""
+    n, re, dt, nt = 64, 10.0, 0.01, 50
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.exact_tgv(x, y, 0.0, re)[:n, :n].copy()
+    g = so.cn_decay(n, dx, dt, re, nt, 4, 4)
+    with spec.SpectralNS2D(n, n, dx, dy, re, kind) as h:
+        h.upload_interior(w0)
+        h.step(dt, nt)
+        ut = h.download()
+    assert np.abs(ut[:n, :n] - g * w0).max() < 1e-12
+    assert abs(g - math.exp(-2 * 16 * nt * dt / re)) < 1e-5  # CN-RK3 vs exact decay
+
+
+def test_gpu_spectral_reference_signature(spec, tmp_path):
+    c = spec.setup(nx=64, ny=64, dt=0.01, tf=0.2, ns=2)
+    ref = so.numerical(c["wn"][1:-1, 1:-1], c["nt"], c["dt"], c["dx"], c["dy"], c["re"],
+                       so.HYBRID)
+    un = spec.numerical(c["nx"], c["ny"], c["nt"], c["dx"], c["dy"], c["dt"], c["re"], c["x"],
+                        c["y"], c["wn"], c["ns"], "hybrid", snapshot_dir=str(tmp_path))
+    assert un.shape == (65, 65) and np.abs(un[:64, :64] - ref).max() < 1e-10
+    assert (tmp_path / "vm1.txt").exists() and (tmp_path / "vm2.txt").exists()
+
+
+def test_gpu_spectral_argument_errors(spec):
+    from cfd_julia_amd import _lib
+
+    dx = 2 * math.pi / 64
+    with pytest.raises(_lib.ArgumentError):
+        spec.SpectralNS2D(64, 32, dx, dx, 1000.0)  # ky = kx aliasing: square only
+    with pytest.raises(_lib.ArgumentError):
+        spec.SpectralNS2D(63, 63, dx, dx, 1000.0)  # odd nx

@@ -127,3 +127,33 @@ def test_cpu_mirror_modules_import():
     from cfd_julia_amd import common, fft_p, fft_s, vm  # noqa: F401
 
     assert callable(fft_s.ps_spectral) and callable(vm.numerical)
+
+
+# ---- spectral-space solvers (hybrid.jl, pseudospectral_23/32_rule.jl) ------------------------
+@pytest.mark.parametrize("kind", [0, 1, 2])
+def test_spectral_oracle_tgv_scheme_decay(kind):
+    """Taylor-Green has J(w, psi) = 0: each solver reproduces the CN-RK3 decay exactly."""
+    from oracle import spectral_oracle as so
+
+    n, re, dt, nt = 32, 10.0, 0.01, 20
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.exact_tgv(x, y, 0.0, re)[:n, :n].copy()
+    w = so.numerical(w0, nt, dt, dx, dy, re, kind)
+    assert np.abs(w - so.cn_decay(n, dx, dt, re, nt, 4, 4) * w0).max() < 1e-12
+
+
+def test_spectral_oracle_jacobians_agree():
+    """Band-limited input: the 2/3- and 3/2-rule products are exact (equal to round-off);
+    the hybrid's FD Arakawa Jacobian converges to them at second order."""
+    from oracle import spectral_oracle as so
+    from tests.golden.make_golden import smooth_field
+
+    errs = []
+    for n in (32, 64):
+        dx, dy, _, _ = vo.vm_grid(n, n)
+        wf = so.to_spectral(smooth_field(n, n, 3, 5))
+        k2 = so.wavespace(n, n, dx, dy)
+        j = [so.to_physical(so.JACOBIANS[k](wf, k2, dx, dy)) for k in (0, 1, 2)]
+        assert np.abs(j[1] - j[2]).max() < 1e-12 * np.abs(j[1]).max()
+        errs.append(np.abs(j[0] - j[1]).max())
+    assert 3.0 < errs[0] / errs[1] < 5.0  # O(dx^2)
