@@ -92,4 +92,40 @@ function fps(nx, ny, Δx, Δy, u, e, data, data1, f, s, ε=1e-6)
     return nothing
 end
 
+"hybrid.jl:14-86 / pseudospectral_*.jl:13-89 on the GPU; kind = 0 hybrid, 1 2/3 rule, 2 3/2 rule."
+function spectral_numerical(nx, ny, nt, Δx, Δy, Δt, re, x, y, wn, ns; kind=0, ε=1e-6, device=-1)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    check(ccall((:cfdj_spec_create, libcfdj), Cint,
+                (Cint, Cint, Cdouble, Cdouble, Cdouble, Cdouble, Cint, Cint, Ptr{Ptr{Cvoid}}),
+                nx, ny, Δx, Δy, re, ε, kind, device, h), "cfdj_spec_create")
+    ut = Array{Float64}(undef, nx + 1, ny + 1)
+    try
+        check(ccall((:cfdj_spec_upload, libcfdj), Cint, (Ptr{Cvoid}, Ptr{Cdouble}, Clong),
+                    h[], wn, size(wn, 1)), "cfdj_spec_upload")
+        freq = nt ÷ ns
+        m = 1
+        for k ∈ 1:nt
+            check(ccall((:cfdj_spec_step, libcfdj), Cint, (Ptr{Cvoid}, Cdouble, Cint),
+                        h[], Δt, 1), "cfdj_spec_step")
+            if mod(k, freq) == 0
+                @show k
+                check(ccall((:cfdj_spec_download, libcfdj), Cint,
+                            (Ptr{Cvoid}, Ptr{Cdouble}, Clong), h[], ut, size(ut, 1)),
+                      "cfdj_spec_download")
+                open("vm$m.txt", "w") do io
+                    for j ∈ 1:ny + 1, i ∈ 1:nx + 1
+                        write(io, "$(x[i]) $(y[j]) $(ut[i, j])\n")
+                    end
+                end
+                m += 1
+            end
+        end
+        check(ccall((:cfdj_spec_download, libcfdj), Cint, (Ptr{Cvoid}, Ptr{Cdouble}, Clong),
+                    h[], ut, size(ut, 1)), "cfdj_spec_download")
+    finally
+        ccall((:cfdj_spec_destroy, libcfdj), Cvoid, (Ptr{Cvoid},), h[])
+    end
+    return ut
+end
+
 end # module
