@@ -310,25 +310,33 @@ struct cfdj_vm {
   void poisson_schur(const std::vector<const double*>& src, bool neg) {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
-    const size_t colb = (size_t)rows * sizeof(double2);
+    auto schur_args = [&](const Slab& s) {
+      SchurArgs sa = schur.args(s.X, T, s.rank, out_scale, ny);
+      sa.tile8 = 1;
+      return sa;
+    };
     std::vector<FusedPoissonArgs> a;
-    for (size_t i = 0; i < slabs.size(); ++i)
+    for (size_t i = 0; i < slabs.size(); ++i) {
       a.push_back(fused.args(sym, src[i], slabs[i].psi, slabs[i].X, slabs[i].X, rows,
                              slabs[i].rank, nranks, neg));
+      a.back().tile8 = 1;  // 8-mode tiles: whole-line row writes, shared column reads
+    }
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_FWD);
       launch_fused_poisson_pass(0, ai, stream);
       tend();
     }
+    // column m = 0 (packed DC / Nyquist) of the tiled spectrum: element j at 8 j
     tbegin(CFDJ_K_COMM);
     for (auto& s : slabs)
-      CFDJ_HIP(hipMemcpyAsync(G + s.row0, s.X, colb, hipMemcpyDeviceToDevice, stream));
+      CFDJ_HIP(hipMemcpy2DAsync(G + s.row0, sizeof(double2), s.X, 8 * sizeof(double2),
+                                sizeof(double2), rows, hipMemcpyDeviceToDevice, stream));
     if (mode == Mode::Rccl)
       CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, stream));
     tend();
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
-      launch_schur_pass(0, schur.args(s.X, T, s.rank, out_scale, ny), stream);
+      launch_schur_pass(0, schur_args(s), stream);
       tend();
     }
     if (mode == Mode::Rccl) {
@@ -356,12 +364,13 @@ struct cfdj_vm {
     tend();
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
-      launch_schur_pass(1, schur.args(s.X, T, s.rank, out_scale, ny), stream);
+      launch_schur_pass(1, schur_args(s), stream);
       tend();
     }
     tbegin(CFDJ_K_COMM);
     for (auto& s : slabs)
-      CFDJ_HIP(hipMemcpyAsync(s.X, G + s.row0, colb, hipMemcpyDeviceToDevice, stream));
+      CFDJ_HIP(hipMemcpy2DAsync(s.X, 8 * sizeof(double2), G + s.row0, sizeof(double2),
+                                sizeof(double2), rows, hipMemcpyDeviceToDevice, stream));
     tend();
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_INV);

@@ -130,6 +130,7 @@ struct FusedPoissonArgs {
   double2* H;           // (nx/2) x rows packed half spectrum, column-major
   double2* C;           // column-pass buffer (kb columns of ny)
   double2* Cout;        // column-pass output (nullptr: in place into C)
+  int tile8;            // row passes: spectrum in 8-mode tiles (Schur y-slab path)
   int rot;              // column-pass output rotated: element y stored at (y - rot) mod ny
                         // (one GPU only; the FFT-fused stage kernel reads row pairs
                         // y+1, y+2 as one aligned segment, vm_fused.hip)
@@ -186,6 +187,7 @@ struct SchurArgs {
   const double2* tw;    // exp(-2 pi i k / (2 rl)), k < 2 rl
   double cc, inv_dy2, out_scale, inv_ny;
   int rl, L, P, rank;
+  int tile8;            // H in 8-mode tiles (sidx in poisson_fft.hip), else column-major
 };
 bool schur_supported(int rl);
 void launch_schur_pass(int pass, const SchurArgs& a, hipStream_t st);  // 0 traces, 1 solve

@@ -267,6 +267,7 @@ struct Fused {
     a.C = C;
     a.Cout = nullptr;
     a.rot = 0;
+    a.tile8 = 0;
     a.kb = (nx / 2) / nranks;
     a.m0 = rank * a.kb;
     int lg = 0;
@@ -355,7 +356,7 @@ struct SchurTables {
       const ld th = log1pl(x + sqrtl(x * (x + 2.0L)));
       const ld den = expm1l(-2.0L * rl * th);
       for (int j = 0; j <= rl; ++j)
-        hg[(size_t)m * (rl + 1) + j] =
+        hg[(((size_t)(m >> 3)) * (rl + 1) + j) * 8 + (m & 7)] =  // 8-mode tiles
             (double)(expl(-(ld)j * th) * (expm1l(-2.0L * (ld)(rl - j) * th) / den));
     }
     e = dalloc<double>(L);
@@ -398,6 +399,7 @@ struct SchurTables {
     a.L = L;
     a.P = P;
     a.rank = rank;
+    a.tile8 = 0;
     return a;
   }
 };

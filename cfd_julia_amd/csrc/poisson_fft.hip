@@ -58,6 +58,16 @@ __device__ __forceinline__ void pair_index(int e, int& qq, int& m) {
   m = ((e >> 4) / C::XR) * 16 + (e & 15);
 }
 
+// Element (m, y) of a half spectrum with `M` rows: column-major (m M + y) or, for the
+// substructured y-slab path, in 8-mode tiles (((m/8) M + y) 8 + m%8): a row's modes are
+// whole 128-B lines, and the Schur kernels' column reads of 8 neighbouring modes share
+// them in L2 (TILE = true).
+template <bool TILE>
+__device__ __forceinline__ size_t sidx(int m, int y, int M) {
+  if constexpr (TILE) return ((((size_t)(m >> 3)) * M + y) << 3) + (m & 7);
+  else return (size_t)m * M + y;
+}
+
 // Prefetch loads use a wave-uniform base pointer and unsigned 32-bit element offsets, so
 // each load needs one offset VGPR (global_load ... saddr) instead of a 64-bit address pair.
 template <int L>
@@ -73,7 +83,7 @@ __device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __res
     for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[(unsigned)in_pos<L, 0>(tid, b, r)];
 }
 
-template <int L>
+template <int L, bool TILE>
 __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
@@ -113,11 +123,11 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
       pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
       const double2* bq = lds + qq * P::ROWSTRIDE;
       const double2 Zm = bq[padx(m)];
-      double2* Hrow = H + y0 + qq;
+      const int y = y0 + qq;
       if (m == 0) {
-        Hrow[0] = make_double2(Zm.x + Zm.y, Zm.x - Zm.y);
+        H[sidx<TILE>(0, y, M)] = make_double2(Zm.x + Zm.y, Zm.x - Zm.y);
         const double2 Zh = bq[padx(L / 2)];  // X[L/2] = E + W^{L/2} O, W^{L/2} = -i
-        Hrow[(size_t)(L / 2) * M] = make_double2(Zh.x, -Zh.y);
+        H[sidx<TILE>(L / 2, y, M)] = make_double2(Zh.x, -Zh.y);
       } else {
         const double2 Zp = bq[padx(L - m)];
         const double2 Zc = cconj(Zp);
@@ -125,9 +135,9 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
         const double2 D = csub(Zm, Zc);                       // = 2i O[m]
         const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
         const double2 WO = cmul(twN.w(m), O);
-        Hrow[(size_t)m * M] = cadd(E, WO);
+        H[sidx<TILE>(m, y, M)] = cadd(E, WO);
         // X[L-m] = conj(E[m]) + W^{L-m} conj(O[m]) = conj(E[m] - W^m O[m])
-        Hrow[(size_t)(L - m) * M] = cconj(csub(E, WO));
+        H[sidx<TILE>(L - m, y, M)] = cconj(csub(E, WO));
       }
     }
     __syncthreads();  // LDS is rewritten by the next item
@@ -276,22 +286,24 @@ struct InvLoads {
   double2 xm[RowCfg<L>::PAIRS], xp[RowCfg<L>::PAIRS];
   double2 xh;  // X[L/2] for the thread that owns m = 0
 };
-template <int L>
+template <int L, bool TILE>
 __device__ __forceinline__ void load_inv(InvLoads<L>& ld, const double2* __restrict__ H, int M,
                                          int y0) {
   using C = RowCfg<L>;
-  const double2* base = H + __builtin_amdgcn_readfirstlane(y0);
+  // uniform row offset in the base pointer, 32-bit per-lane offsets (sidx(m, y0 + qq) =
+  // sidx(m, qq) + sidx(0, y0) in both layouts)
+  const double2* base = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
 #pragma unroll
   for (int i = 0; i < C::PAIRS; ++i) {
     int qq, m;
     pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
-    ld.xm[i] = base[(unsigned)(m * M + qq)];
-    ld.xp[i] = base[(unsigned)(((L - m) & (L - 1)) * M + qq)];  // m = 0: unused
-    if (m == 0) ld.xh = base[(unsigned)((L / 2) * M + qq)];
+    ld.xm[i] = base[(unsigned)sidx<TILE>(m, qq, M)];
+    ld.xp[i] = base[(unsigned)sidx<TILE>((L - m) & (L - 1), qq, M)];  // m = 0: unused
+    if (m == 0) ld.xh = base[(unsigned)sidx<TILE>(L / 2, qq, M)];
   }
 }
 
-template <int L>
+template <int L, bool TILE>
 __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_inv_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_inv_kernel(
   twL.fill(twL_);
   twN.fill(twN_);
   InvLoads<L> nxt;
-  if (rg.count > 0) load_inv<L>(nxt, H, M, rg.first * C::XR);
+  if (rg.count > 0) load_inv<L, TILE>(nxt, H, M, rg.first * C::XR);
   __syncthreads();
   for (int it = 0; it < rg.count; ++it) {
     const int y0 = (rg.first + it * rg.stride) * C::XR;
@@ -332,7 +344,7 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_inv_kernel(
         bq[padx(L - m)] = make_double2(S.x + D.y, D.x - S.y);
       }
     }
-    if (it + 1 < rg.count) load_inv<L>(nxt, H, M, y0 + rg.stride * C::XR);
+    if (it + 1 < rg.count) load_inv<L, TILE>(nxt, H, M, y0 + rg.stride * C::XR);
     __syncthreads();
 
     double2 v[16];
@@ -363,12 +375,21 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
                           sizeof(TwLds<2 * L>);
   const int per_cu = (160 * 1024) / row_lds;
   const dim3 grid(persistent_grid(a.ncu, per_cu, a.rows / C::XR));
-  if (pass == 0)
-    hipLaunchKernelGGL(rows_fwd_kernel<L>, grid, dim3(C::THREADS), 0, st, a.f, a.H, a.rows,
-                       a.twL, a.twN);
-  else
-    hipLaunchKernelGGL(rows_inv_kernel<L>, grid, dim3(C::THREADS), 0, st, a.H, a.s, a.rows,
-                       a.twL, a.twN);
+  if (pass == 0) {
+    if (a.tile8)
+      hipLaunchKernelGGL((rows_fwd_kernel<L, true>), grid, dim3(C::THREADS), 0, st, a.f, a.H,
+                         a.rows, a.twL, a.twN);
+    else
+      hipLaunchKernelGGL((rows_fwd_kernel<L, false>), grid, dim3(C::THREADS), 0, st, a.f, a.H,
+                         a.rows, a.twL, a.twN);
+  } else {
+    if (a.tile8)
+      hipLaunchKernelGGL((rows_inv_kernel<L, true>), grid, dim3(C::THREADS), 0, st, a.H, a.s,
+                         a.rows, a.twL, a.twN);
+    else
+      hipLaunchKernelGGL((rows_inv_kernel<L, false>), grid, dim3(C::THREADS), 0, st, a.H, a.s,
+                         a.rows, a.twL, a.twN);
+  }
 }
 
 template <int M>
@@ -399,7 +420,7 @@ bool fused_poisson_supported(int nx, int ny, int rows) {
 }
 
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  const bool ok = pass == 1 ? fused_poisson_supported(a.nx, a.ny, a.rows) && a.kb >= 1 &&
+  const bool ok = pass == 1 ? !a.tile8 && fused_poisson_supported(a.nx, a.ny, a.rows) && a.kb >= 1 &&
                                  (1 << a.rl_log2) <= a.ny &&
                                  (a.rot == 0 || (1 << a.rl_log2) == a.ny)
                            : fused_rows_supported(a.nx, a.rows);

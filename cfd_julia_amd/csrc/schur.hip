@@ -27,49 +27,13 @@ namespace {
 
 __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
 
-// Sum of three complex values over the workgroup (result valid in thread 0).
-template <int T>
-__device__ __forceinline__ void block_sum3(double2& a, double2& b, double2& c) {
-  constexpr int W = T / 64 > 0 ? T / 64 : 1;
-  __shared__ double red[6][W];
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) {
-    a.x += __shfl_xor(a.x, o);
-    a.y += __shfl_xor(a.y, o);
-    b.x += __shfl_xor(b.x, o);
-    b.y += __shfl_xor(b.y, o);
-    c.x += __shfl_xor(c.x, o);
-    c.y += __shfl_xor(c.y, o);
-  }
-  const int wv = threadIdx.x / 64, ln = threadIdx.x % 64;
-  if (ln == 0) {
-    red[0][wv] = a.x;
-    red[1][wv] = a.y;
-    red[2][wv] = b.x;
-    red[3][wv] = b.y;
-    red[4][wv] = c.x;
-    red[5][wv] = c.y;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    a = b = c = make_double2(0.0, 0.0);
-    for (int w = 0; w < W; ++w) {
-      a.x += red[0][w];
-      a.y += red[1][w];
-      b.x += red[2][w];
-      b.y += red[3][w];
-      c.x += red[4][w];
-      c.y += red[5][w];
-    }
-  }
-}
-
 // Odd extension of interior rows 1..RL-1 of a slab column (length M2 = 2 RL), stage-0
 // order; `fix1` / `fixn` are subtracted from rows 1 and RL-1 (Dirichlet data of pass 1).
 // Returns the sum of the loaded interior values in `fs`.
 template <int M2>
 __device__ __forceinline__ void load_odd(double2 (&v)[16], const double2* __restrict__ col,
-                                         int tid, double2 fix1, double2 fixn, double2& fs) {
+                                         int cs, int tid, double2 fix1, double2 fixn,
+                                         double2& fs) {
   constexpr int RL = M2 / 2;
   constexpr int R0 = Plan<M2>::radix(0);
 #pragma unroll
@@ -80,7 +44,7 @@ __device__ __forceinline__ void load_odd(double2 (&v)[16], const double2* __rest
       const int i = j < RL ? j : M2 - j;  // interior row of this element
       double2 x = make_double2(0.0, 0.0);
       if (i != 0 && i != RL) {
-        x = col[i];
+        x = col[(size_t)i * cs];
         if (i == 1) x = csub(x, fix1);
         if (i == RL - 1) x = csub(x, fixn);
         if (j < RL) fs = cadd(fs, x);
@@ -102,27 +66,63 @@ __device__ __forceinline__ double2 dst_divide(double2 y, int k, double em, doubl
   return make_double2(y.x / lam, y.y / lam);
 }
 
-// Pass 0: one workgroup per x-mode.  The zero-Dirichlet interior solution's boundary values
-// are rows of the interior Green's function, (T_int^-1)[1, j] = -dy^2 gL(j) and
-// (T_int^-1)[n, j] = -dy^2 gL(rl - j) (gL: the homogeneous solution with gL(0) = 1,
-// gL(rl) = 0, tabulated on the host in long double), so the traces are two dot products
-// over the slab column -- one streaming read, no transform.
+// Column m of the slab spectrum: base pointer and element stride (column-major, or the
+// 8-mode tiles of poisson_fft.hip's sidx: element (m, j) at ((m/8) rl + j) 8 + m%8).
+__device__ __forceinline__ double2* slab_col(const SchurArgs& a, int m, int& cs) {
+  cs = a.tile8 ? 8 : 1;
+  return a.H + (a.tile8 ? ((((size_t)(m >> 3)) * a.rl) << 3) + (m & 7) : (size_t)m * a.rl);
+}
+
+// Pass 0: one workgroup per 8-mode tile of the spectrum (8 x-modes, element (m, j) at
+// ((m/8) rl + j) 8 + m%8, rows_fwd_kernel's tiled output), so every wavefront load is 8
+// whole rows of the tile, 1 KB contiguous.  The zero-Dirichlet interior solution's
+// boundary values are rows of the interior Green's function, (T_int^-1)[1, j] =
+// -dy^2 gL(j) and (T_int^-1)[n, j] = -dy^2 gL(rl - j) (gL: the homogeneous solution with
+// gL(0) = 1, gL(rl) = 0, tabulated on the host in long double, same tiling), so the
+// traces are two dot products over the slab column -- one streaming read, no transform.
+// Lane = (row r, mode mi): mi = tid % 8, rows j = 1 + tid/8, + 32, ...
 constexpr int kTraceThreads = 256;
 __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurArgs a) {
-  const int m = 1 + xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = xcd_remap(blockIdx.x, gridDim.x);  // tile: modes 8 tb .. 8 tb + 7
+  const int mi = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+  const int m = 8 * tb + mi;
   const int rl = a.rl;
-  const double2* col = a.H + (size_t)m * rl;
-  const double* g = a.g + (size_t)m * (rl + 1);
+  const double2* tile = a.H + (((size_t)tb * rl) << 3);
+  const double* g = a.g + (((size_t)tb * (rl + 1)) << 3) + mi;
   double2 t1 = make_double2(0.0, 0.0), tn = t1, fs = t1;
-  for (int j = 1 + threadIdx.x; j < rl; j += kTraceThreads) {
-    const double2 f = col[j];
-    t1 = cadd(t1, cscale(f, g[j]));
-    tn = cadd(tn, cscale(f, g[rl - j]));
+  for (int j = 1 + r0; j < rl; j += kTraceThreads / 8) {
+    const double2 f = tile[((size_t)j << 3) + mi];
+    t1 = cadd(t1, cscale(f, g[(size_t)j << 3]));
+    tn = cadd(tn, cscale(f, g[(size_t)(rl - j) << 3]));
     fs = cadd(fs, f);
   }
-  block_sum3<kTraceThreads>(t1, tn, fs);
-  if (threadIdx.x == 0) {
-    const double2 fsep = col[0];
+  // sum over the 8 row lanes of a wavefront with the same mode, then over the 4 waves
+#pragma unroll
+  for (int o = 8; o < 64; o <<= 1) {
+    t1.x += __shfl_xor(t1.x, o);
+    t1.y += __shfl_xor(t1.y, o);
+    tn.x += __shfl_xor(tn.x, o);
+    tn.y += __shfl_xor(tn.y, o);
+    fs.x += __shfl_xor(fs.x, o);
+    fs.y += __shfl_xor(fs.y, o);
+  }
+  constexpr int W = kTraceThreads / 64;
+  __shared__ double2 red[3][W][8];
+  const int wv = threadIdx.x / 64, ln = threadIdx.x % 64;
+  if (ln < 8) {
+    red[0][wv][ln] = t1;
+    red[1][wv][ln] = tn;
+    red[2][wv][ln] = fs;
+  }
+  __syncthreads();
+  if (threadIdx.x < 8 && m >= 1) {
+    t1 = tn = fs = make_double2(0.0, 0.0);
+    for (int w = 0; w < W; ++w) {
+      t1 = cadd(t1, red[0][w][mi]);
+      tn = cadd(tn, red[1][w][mi]);
+      fs = cadd(fs, red[2][w][mi]);
+    }
+    const double2 fsep = tile[mi];
     const double mdy2 = -1.0 / a.inv_dy2;
     double2* out = a.T + ((size_t)a.rank * a.L + m) * 4;
     out[0] = fsep;
@@ -140,7 +140,8 @@ __global__ __launch_bounds__(Plan<M2>::T) void schur_solve_kernel(const SchurArg
   const TwGlobal<M2> tw{a.tw};
   const int tid = threadIdx.x;
   const int m = 1 + xcd_remap(blockIdx.x, gridDim.x);
-  double2* col = a.H + (size_t)m * RL;
+  int cs;
+  double2* col = slab_col(a, m, cs);
 
   // separator values s_rank, s_rank+1 from every rank's traces (P <= a few dozen)
   double2 sp = make_double2(0.0, 0.0), sq = sp, fb = sp;
@@ -157,7 +158,7 @@ __global__ __launch_bounds__(Plan<M2>::T) void schur_solve_kernel(const SchurArg
 
   double2 v[16];
   double2 fs = make_double2(0.0, 0.0);
-  load_odd<M2>(v, col, tid, cscale(sp, a.inv_dy2), cscale(sq, a.inv_dy2), fs);
+  load_odd<M2>(v, col, cs, tid, cscale(sp, a.inv_dy2), cscale(sq, a.inv_dy2), fs);
   stage_regs<M2, 0, -1>(v, tid, tw);
   lds_write<M2, 0>(lds, v, tid);
   __syncthreads();
@@ -182,7 +183,8 @@ __global__ __launch_bounds__(Plan<M2>::T) void schur_solve_kernel(const SchurArg
       const int j = out_pos<M2, SL>(tid, b, r);
       if (j >= 1 && j < RL) {
         const double2 x = w[b * RLAST + r];
-        col[j] = make_double2((x.x * (1.0 / M2) + cst.x) * s, (x.y * (1.0 / M2) + cst.y) * s);
+        col[(size_t)j * cs] =
+            make_double2((x.x * (1.0 / M2) + cst.x) * s, (x.y * (1.0 / M2) + cst.y) * s);
       }
     }
   if (tid == 0) col[0] = make_double2((sp.x + cst.x) * s, (sp.y + cst.y) * s);
@@ -219,7 +221,7 @@ template <int M2>
 void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
   const dim3 grid(a.L - 1), block(Plan<M2>::T);
   if (pass == 0)
-    hipLaunchKernelGGL(schur_trace_kernel, grid, dim3(kTraceThreads), 0, st, a);
+    hipLaunchKernelGGL(schur_trace_kernel, dim3(a.L / 8), dim3(kTraceThreads), 0, st, a);
   else
     hipLaunchKernelGGL(schur_solve_kernel<M2>, grid, block, 0, st, a);
 }
@@ -230,7 +232,8 @@ void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
 bool schur_supported(int rl) { return rl == 512 || rl == 1024 || rl == 2048 || rl == 4096; }
 
 void launch_schur_pass(int pass, const SchurArgs& a, hipStream_t st) {
-  if (!schur_supported(a.rl) || a.L < 2 || a.P < 1 || a.rank < 0 || a.rank >= a.P)
+  if (!schur_supported(a.rl) || a.L < 8 || a.L % 8 != 0 || !a.tile8 || a.P < 1 ||
+      a.rank < 0 || a.rank >= a.P)
     throw Error{CFDJ_ERR_ARG, "substructured Poisson: unsupported slab"};
   switch (a.rl) {
     case 512: launch_schur_n<1024>(pass, a, st); break;
