@@ -177,17 +177,18 @@ void launch_fused_stage(int stage, const FusedStageParams& p, hipStream_t st);
 // per rank (row 0 of each slab); interior blocks by DST-I (odd-extension FFT of length
 // 2 rl in LDS), separators by a P x P circulant system from the gathered traces.
 struct SchurArgs {
-  double2* H;           // this rank's column-major half spectrum, pitch rl (in place)
+  double2* H;           // this rank's half spectrum in 8-mode tiles, rl rows (in place)
   double2* T;           // [P][L][4] traces of every rank: f_sep, t_1, t_n, column sum
-  const double* e;      // e_m = d_m + cc (exact sum, rounded once), m < L
-  const double* q;      // q_k = 1 - cos(pi k / rl), k <= rl
   const double* cinv;   // [L][P] first row of the inverse circulant separator system
   const double* corr;   // [L] 1/D_ref(m, 0) - 1/e_m (the reference's ky[1] = eps)
-  const double* g;      // [L][rl + 1] interior homogeneous solution gL (gL(0)=1, gL(rl)=0)
-  const double2* tw;    // exp(-2 pi i k / (2 rl)), k < 2 rl
-  double cc, inv_dy2, out_scale, inv_ny;
+  const double* g;      // trace Green's function gL(j), j = 0..rl, in 8-mode tiles
+  const double* tip;    // [L][32] inverse pivots of a 31-row chunk (system scaled by dy^2)
+  const double* tg;     // [L][33] chunk homogeneous solution g(i), g(0) = 1, g(32) = 0
+  const double* tA;     // [L] interface off-diagonal g(31)
+  const double* tiq;    // [L][K] inverse pivots of the K-1 interface system
+  double inv_dy2, dy2, out_scale, inv_ny;
   int rl, L, P, rank;
-  int tile8;            // H in 8-mode tiles (sidx in poisson_fft.hip), else column-major
+  int tile8;            // H in 8-mode tiles (sidx in poisson_fft.hip); required
 };
 bool schur_supported(int rl);
 void launch_schur_pass(int pass, const SchurArgs& a, hipStream_t st);  // 0 traces, 1 solve

@@ -297,41 +297,49 @@ struct Fused {
 
 // Tables of the substructured y-slab solve (schur.hip), built in long double.
 struct SchurTables {
-  int rl = 0, L = 0, P = 0;
-  double cc = 0, inv_dy2 = 0;
-  double *e = nullptr, *q = nullptr, *cinv = nullptr, *corr = nullptr, *g = nullptr;
-  double2* tw = nullptr;
-  bool ready() const { return e != nullptr; }
+  static constexpr int kC = 32;  // chunk rows of the interior solve (schur.hip kChunk)
+  int rl = 0, L = 0, P = 0, K = 0;
+  double inv_dy2 = 0, dy2 = 0;
+  double *cinv = nullptr, *corr = nullptr, *g = nullptr;
+  double *tip = nullptr, *tg = nullptr, *tA = nullptr, *tiq = nullptr;
+  bool ready() const { return cinv != nullptr; }
   void init(int nx, int ny, double dx, double dy, double eps, int nranks) {
     typedef long double ld;
     const ld pi = 3.141592653589793238462643383279502884L;
     P = nranks;
     rl = ny / nranks;
     L = nx / 2;
+    K = rl / kC;
     const double aa = -2.0 / (dx * dx) - 2.0 / (dy * dy);
     const double bb = 2.0 / (dx * dx);
-    cc = 2.0 / (dy * dy);
-    inv_dy2 = 1.0 / (dy * dy);
+    const double cc = 2.0 / (dy * dy);
+    inv_dy2 = 1.0 / (dy * dy);  // the off-diagonal: cc == 2 inv_dy2 exactly
+    dy2 = (double)(1.0L / (ld)inv_dy2);
     const std::vector<double> kx = kx_table(nx, eps);
     const double ce = std::cos(kx[0]);  // reference cos(ky[1]) = cos(eps)
-    std::vector<double> he(L), hq(rl + 1), hc((size_t)L * P, 0.0), hr(L, 0.0);
+    std::vector<double> hc((size_t)L * P, 0.0), hr(L, 0.0);
     std::vector<double> hg((size_t)L * (rl + 1), 0.0);
+    std::vector<double> hip((size_t)L * kC, 0.0), htg((size_t)L * (kC + 1), 0.0), hA(L, 0.0),
+        hiq((size_t)L * K, 0.0);
     std::vector<ld> s2(rl), qk(rl + 1);
     for (int k = 0; k <= rl; ++k) {
       const ld sn = sinl(pi * (ld)k / (ld)(2 * rl));
       qk[k] = 2.0L * sn * sn;  // 1 - cos(pi k / rl) without cancellation
-      hq[k] = (double)qk[k];
     }
     for (int k = 1; k < rl; ++k) {
       const ld sn = sinl(pi * (ld)k / (ld)rl);
       s2[k] = sn * sn;
     }
     const ld dy4 = ((ld)dy * (ld)dy) * ((ld)dy * (ld)dy);
-    for (int m = 0; m < L; ++m) {
+    const ld o = (ld)inv_dy2;
+    // homogeneous solution with h(0) = 1, h(n) = 0 of psi[j-1] + psi[j+1] - (2 + eps) psi[j]
+    // = 0, cosh th = 1 + eps/2: e^{-j th} expm1(-2(n-j) th) / expm1(-2 n th)
+    auto homog = [](ld th, int n, int j) {
+      return expl(-(ld)j * th) * (expm1l(-2.0L * (ld)(n - j) * th) / expm1l(-2.0L * n * th));
+    };
+    for (int m = 1; m < L; ++m) {  // m = 0: packed DC / Nyquist column, gathered-column FFT
       const double dm = aa + bb * std::cos(kx[m]);  // Common.jl:120 order (no FMA)
       const ld em = (ld)dm + (ld)cc;                // constant-mode eigenvalue, exact sum
-      he[m] = (double)em;
-      if (m == 0) continue;  // packed DC / Nyquist column: gathered-column FFT
       ld a1 = 0.0L, an = 0.0L;
       for (int k = 1; k < rl; ++k) {
         const ld t = s2[k] / (em - (ld)cc * qk[k]);
@@ -350,56 +358,68 @@ struct SchurTables {
       }
       const double dref = (aa + bb * std::cos(kx[m])) + cc * ce;  // reference D(m, 0)
       hr[m] = (double)(1.0L / (ld)dref - 1.0L / em);
-      // gL(j) = sinh((rl-j) th) / sinh(rl th), cosh th = 1 + x, x = -e_m dy^2 / 2 (>= 0),
-      // in the overflow-free form e^{-j th} expm1(-2(rl-j) th) / expm1(-2 rl th)
-      const ld x = -em * ((ld)dy * (ld)dy) / 2.0L;
+      // the operator scaled by dy^2 (1/o): off-diagonal 1, diagonal -(2 + ep), ep = -e_m/o
+      const ld ep = -em / o;
+      const ld x = ep / 2.0L;
       const ld th = log1pl(x + sqrtl(x * (x + 2.0L)));
-      const ld den = expm1l(-2.0L * rl * th);
-      for (int j = 0; j <= rl; ++j)
-        hg[(((size_t)(m >> 3)) * (rl + 1) + j) * 8 + (m & 7)] =  // 8-mode tiles
-            (double)(expl(-(ld)j * th) * (expm1l(-2.0L * (ld)(rl - j) * th) / den));
+      for (int j = 0; j <= rl; ++j)  // trace pass: gL over the slab, 8-mode tiles
+        hg[(((size_t)(m >> 3)) * (rl + 1) + j) * 8 + (m & 7)] = (double)homog(th, rl, j);
+      // chunk Thomas pivots p_i = -(1 + s_i): s_1 = 1 + ep, s_i = (s(1 + ep) + ep)/(1 + s)
+      ld sv = 1.0L + ep;
+      for (int i = 1; i < kC; ++i) {
+        if (i > 1) sv = (sv * (1.0L + ep) + ep) / (1.0L + sv);
+        hip[(size_t)m * kC + (i - 1)] = (double)(-1.0L / (1.0L + sv));
+      }
+      std::vector<ld> gc(kC + 1);
+      for (int i = 0; i <= kC; ++i) {
+        gc[i] = homog(th, kC, i);
+        htg[(size_t)m * (kC + 1) + i] = (double)gc[i];
+      }
+      // interface system A v_{k-1} + B v_k + A v_{k+1}: A = g(C-1), B = -(2 + ep) + 2 g(1)
+      const ld A = gc[kC - 1], B = -(2.0L + ep) + 2.0L * gc[1];
+      hA[m] = (double)A;
+      ld q = B;
+      for (int k = 1; k < K; ++k) {
+        if (k > 1) q = B - A * A / q;
+        hiq[(size_t)m * K + (k - 1)] = (double)(1.0L / q);
+      }
     }
-    e = dalloc<double>(L);
-    q = dalloc<double>(rl + 1);
-    cinv = dalloc<double>((size_t)L * P);
-    corr = dalloc<double>(L);
-    g = dalloc<double>(hg.size());
-    CFDJ_HIP(hipMemcpy(g, hg.data(), hg.size() * sizeof(double), hipMemcpyHostToDevice));
-    CFDJ_HIP(hipMemcpy(e, he.data(), L * sizeof(double), hipMemcpyHostToDevice));
-    CFDJ_HIP(hipMemcpy(q, hq.data(), (rl + 1) * sizeof(double), hipMemcpyHostToDevice));
-    CFDJ_HIP(hipMemcpy(cinv, hc.data(), hc.size() * sizeof(double), hipMemcpyHostToDevice));
-    CFDJ_HIP(hipMemcpy(corr, hr.data(), L * sizeof(double), hipMemcpyHostToDevice));
-    tw = twiddle_table(2 * rl);
+    cinv = upload(hc);
+    corr = upload(hr);
+    g = upload(hg);
+    tip = upload(hip);
+    tg = upload(htg);
+    tA = upload(hA);
+    tiq = upload(hiq);
+  }
+  static double* upload(const std::vector<double>& h) {
+    double* d = dalloc<double>(h.size());
+    CFDJ_HIP(hipMemcpy(d, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice));
+    return d;
   }
   void destroy() {
-    dfree(e);
-    dfree(q);
-    dfree(cinv);
-    dfree(corr);
-    dfree(g);
-    dfree(tw);
-    e = q = cinv = corr = g = nullptr;
-    tw = nullptr;
+    for (double** p : {&cinv, &corr, &g, &tip, &tg, &tA, &tiq}) dfree(*p);
   }
   SchurArgs args(double2* H, double2* T, int rank, double out_scale, int ny) const {
     SchurArgs a;
     a.H = H;
     a.T = T;
-    a.e = e;
-    a.q = q;
     a.cinv = cinv;
     a.corr = corr;
     a.g = g;
-    a.tw = tw;
-    a.cc = cc;
+    a.tip = tip;
+    a.tg = tg;
+    a.tA = tA;
+    a.tiq = tiq;
     a.inv_dy2 = inv_dy2;
+    a.dy2 = dy2;
     a.out_scale = out_scale;
     a.inv_ny = 1.0 / (double)ny;
     a.rl = rl;
     a.L = L;
     a.P = P;
     a.rank = rank;
-    a.tile8 = 0;
+    a.tile8 = 1;
     return a;
   }
 };

@@ -12,12 +12,14 @@
 //          its separator row f[0] and its column sum;
 //   (the host all-gathers those 4 numbers per mode: 64 B x nx/2 per rank)
 //   pass 1 (schur_solve_kernel): solves the P x P circulant separator system for its two
-//          separator values (precomputed inverse), solves the interior rows 1..rl-1 with
-//          them as Dirichlet data (DST-I = FFT of length 2 rl on the odd extension, in LDS)
-//          and writes psi-hat (plus the constant-mode correction) in place.
+//          separator values (precomputed inverse), then the interior rows 1..rl-1 with
+//          them as Dirichlet data -- a constant-coefficient tridiagonal system per mode,
+//          solved directly in 32-row chunks + a reduced interface system -- and writes
+//          psi-hat (plus the constant-mode correction) in place.
 // The x-modes 0 and nx/2 (packed in column 0) are solved separately: the column is gathered
 // and FFT'd along y with the reference symbol (packed_divide_kernel).
-// Host-side tables (long double): e_m, q_k, the circulant inverse, corr -- host_common.hpp.
+// Host-side tables (long double): the circulant inverse, corr, the Green's function of the
+// trace pass, the chunk / interface pivots and homogeneous solutions -- host_common.hpp.
 #pragma clang fp contract(fast)
 #include "fft_lds.hpp"
 
@@ -26,52 +28,6 @@ namespace cfdj {
 namespace {
 
 __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_double2(a.x * s, a.y * s); }
-
-// Odd extension of interior rows 1..RL-1 of a slab column (length M2 = 2 RL), stage-0
-// order; `fix1` / `fixn` are subtracted from rows 1 and RL-1 (Dirichlet data of pass 1).
-// Returns the sum of the loaded interior values in `fs`.
-template <int M2>
-__device__ __forceinline__ void load_odd(double2 (&v)[16], const double2* __restrict__ col,
-                                         int cs, int tid, double2 fix1, double2 fixn,
-                                         double2& fs) {
-  constexpr int RL = M2 / 2;
-  constexpr int R0 = Plan<M2>::radix(0);
-#pragma unroll
-  for (int b = 0; b < 16 / R0; ++b)
-#pragma unroll
-    for (int r = 0; r < R0; ++r) {
-      const int j = in_pos<M2, 0>(tid, b, r);
-      const int i = j < RL ? j : M2 - j;  // interior row of this element
-      double2 x = make_double2(0.0, 0.0);
-      if (i != 0 && i != RL) {
-        x = col[(size_t)i * cs];
-        if (i == 1) x = csub(x, fix1);
-        if (i == RL - 1) x = csub(x, fixn);
-        if (j < RL) fs = cadd(fs, x);
-        else x = make_double2(-x.x, -x.y);
-      }
-      v[b * R0 + r] = x;
-    }
-}
-
-// W_k = Y_k / lambda_k, lambda_k = e_m - cc q_|k| (no cancellation: both terms <= 0);
-// k = 0 and k = RL carry nothing (odd extension).
-template <int M2>
-__device__ __forceinline__ double2 dst_divide(double2 y, int k, double em, double cc,
-                                              const double* __restrict__ q) {
-  constexpr int RL = M2 / 2;
-  if (k == 0 || k == RL) return make_double2(0.0, 0.0);
-  const int kk = k < RL ? k : M2 - k;
-  const double lam = em - cc * q[kk];
-  return make_double2(y.x / lam, y.y / lam);
-}
-
-// Column m of the slab spectrum: base pointer and element stride (column-major, or the
-// 8-mode tiles of poisson_fft.hip's sidx: element (m, j) at ((m/8) rl + j) 8 + m%8).
-__device__ __forceinline__ double2* slab_col(const SchurArgs& a, int m, int& cs) {
-  cs = a.tile8 ? 8 : 1;
-  return a.H + (a.tile8 ? ((((size_t)(m >> 3)) * a.rl) << 3) + (m & 7) : (size_t)m * a.rl);
-}
 
 // Pass 0: one workgroup per 8-mode tile of the spectrum (8 x-modes, element (m, j) at
 // ((m/8) rl + j) 8 + m%8, rows_fwd_kernel's tiled output), so every wavefront load is 8
@@ -132,62 +88,117 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
   }
 }
 
-template <int M2>
-__global__ __launch_bounds__(Plan<M2>::T) void schur_solve_kernel(const SchurArgs a) {
-  using P = Plan<M2>;
-  constexpr int RL = M2 / 2;
-  __shared__ double2 lds[P::PAD];
-  const TwGlobal<M2> tw{a.tw};
-  const int tid = threadIdx.x;
-  const int m = 1 + xcd_remap(blockIdx.x, gridDim.x);
-  int cs;
-  double2* col = slab_col(a, m, cs);
+// Pass 1: the interior rows 1 .. rl-1 of every x-mode m >= 1 with the separator values
+// s_p (row 0) and s_q (row rl, the next slab's row 0) as Dirichlet data, i.e. the
+// tridiagonal system (psi[j-1] + psi[j+1]) / dy^2 + d_m psi[j] = f[j], solved directly
+// (no transform), one workgroup per 8-mode tile:
+//   * rows are cut into K chunks of kChunk rows: chunk k = interface row k C plus the
+//     C - 1 rows after it; thread (mode mi, chunk k) solves its C - 1 rows with zero
+//     boundary values by the Thomas algorithm (tabulated inverse pivots, the system scaled
+//     by dy^2 so the off-diagonal is 1) -- the particular solution u;
+//   * psi = u + v_k g(i) + v_{k+1} g(C - i) on chunk k, g the homogeneous solution with
+//     g(0) = 1, g(C) = 0 (tabulated), v_k = psi at interface row k C (v_0 = s_p, v_K = s_q);
+//   * the interface rows give a K-1 tridiagonal system in v, A v_{k-1} + B v_k + A v_{k+1}
+//     = dy^2 f[kC] - u^{(k-1)}_{C-1} - u^{(k)}_1, solved by one lane per mode (tabulated
+//     inverse pivots).
+// Reads and writes each element once, whole 128-B tile rows per 8 lanes.  All pivots and
+// coefficients are built on the host in long double from e_m = d_m + 2/dy^2 (exact), so
+// the near-singular low modes lose nothing to cancellation (host_common.hpp).
+constexpr int kChunk = 32;
 
-  // separator values s_rank, s_rank+1 from every rank's traces (P <= a few dozen)
+// K chunks per mode, MW modes per workgroup (8 = a whole tile; 4 = half a tile for the
+// 128-chunk slabs, so MW K stays within the 1024-thread / register budget).
+template <int K, int MW>
+__global__ __launch_bounds__(MW * K) void schur_solve_kernel(const SchurArgs a) {
+  constexpr int C = kChunk;
+  constexpr int PER = 8 / MW;  // workgroups per tile
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = lb / PER;
+  const int mi = threadIdx.x % MW, k = threadIdx.x / MW;
+  const int m8 = (lb % PER) * MW + mi;  // mode within the tile
+  const int m = 8 * tb + m8;
+  const bool act = m >= 1;  // m = 0 (packed DC / Nyquist) is solved on the gathered column
+  const int mm = act ? m : 1;
+  double2* tile = a.H + (((size_t)tb * a.rl) << 3) + m8;  // row j at tile[8 j]
+  __shared__ double2 fst[K][MW], lst[K][MW], rint[K][MW], V[K + 1][MW];
+  __shared__ double sip[MW][C], sg[MW][C + 1];
+
+  // this workgroup's pivots and homogeneous solutions into LDS (read in the sweeps)
+  for (int t = threadIdx.x; t < MW * (2 * C + 1); t += MW * K) {
+    const int w = t / (2 * C + 1), r = t % (2 * C + 1);
+    const int mw = 8 * tb + (lb % PER) * MW + w;
+    const int mr = mw >= 1 ? mw : 1;
+    if (r < C) sip[w][r] = a.tip[(size_t)mr * C + r];
+    else sg[w][r - C] = a.tg[(size_t)mr * (C + 1) + (r - C)];
+  }
+
+  // separator values s_rank, s_rank+1 from every rank's traces (as the reference's
+  // periodic circulant), and the constant-mode correction
   double2 sp = make_double2(0.0, 0.0), sq = sp, fb = sp;
-  const double* ci = a.cinv + (size_t)m * a.P;
+  const double* ci = a.cinv + (size_t)mm * a.P;
   for (int qq = 0; qq < a.P; ++qq) {
-    const double2* Tq = a.T + ((size_t)qq * a.L + m) * 4;
-    const double2* Tm = a.T + ((size_t)((qq + a.P - 1) % a.P) * a.L + m) * 4;
+    const double2* Tq = a.T + ((size_t)qq * a.L + mm) * 4;
+    const double2* Tm = a.T + ((size_t)((qq + a.P - 1) % a.P) * a.L + mm) * 4;
     const double2 rhs = csub(Tq[0], cscale(cadd(Tm[2], Tq[1]), a.inv_dy2));
     sp = cadd(sp, cscale(rhs, ci[(qq - a.rank + a.P) % a.P]));
     sq = cadd(sq, cscale(rhs, ci[(qq - a.rank - 1 + 2 * a.P) % a.P]));
     fb = cadd(fb, Tq[3]);
   }
-  const double2 cst = cscale(fb, a.corr[m] * a.inv_ny);
+  const double2 cst = cscale(fb, a.corr[mm] * a.inv_ny);
 
-  double2 v[16];
-  double2 fs = make_double2(0.0, 0.0);
-  load_odd<M2>(v, col, cs, tid, cscale(sp, a.inv_dy2), cscale(sq, a.inv_dy2), fs);
-  stage_regs<M2, 0, -1>(v, tid, tw);
-  lds_write<M2, 0>(lds, v, tid);
+  // chunk rows, scaled by dy^2
+  const double sc = a.dy2;
+  double2 y[C - 1];
+#pragma unroll
+  for (int i = 1; i < C; ++i) y[i - 1] = cscale(tile[(size_t)(k * C + i) << 3], sc);
+  const double2 fint = cscale(tile[(size_t)(k * C) << 3], sc);
+  __syncthreads();  // tables
+
+  // Thomas with zero boundary values: y_i -= y_{i-1} / p_{i-1}; u_i = (y_i - u_{i+1}) / p_i
+  const double* ip = sip[mi];  // 1 / p_i at [i - 1]
+#pragma unroll
+  for (int i = 1; i < C - 1; ++i) y[i] = csub(y[i], cscale(y[i - 1], ip[i - 1]));
+  y[C - 2] = cscale(y[C - 2], ip[C - 2]);
+#pragma unroll
+  for (int i = C - 3; i >= 0; --i) y[i] = cscale(csub(y[i], y[i + 1]), ip[i]);
+  fst[k][mi] = y[0];
+  lst[k][mi] = y[C - 2];
+  rint[k][mi] = fint;
   __syncthreads();
-  run_stages<M2, 1, -1, false>(lds, v, tid, tw);
-  double2 w[16];
-  fwd_to_inv<M2>(v, w);
-  const double em = a.e[m];
-#pragma unroll
-  for (int r = 0; r < 16; ++r) w[r] = dst_divide<M2>(w[r], tid + P::T * r, em, a.cc, a.q);
-  __syncthreads();  // LDS is rewritten by the inverse stage 0
-  stage_regs<M2, 0, 1>(w, tid, tw);
-  lds_write<M2, 0>(lds, w, tid);
-  __syncthreads();
-  run_stages<M2, 1, 1, false>(lds, w, tid, tw);
-  constexpr int SL = P::NSTAGES - 1;
-  constexpr int RLAST = P::radix(SL);
-  const double s = a.out_scale;
-#pragma unroll
-  for (int b = 0; b < 16 / RLAST; ++b)
-#pragma unroll
-    for (int r = 0; r < RLAST; ++r) {
-      const int j = out_pos<M2, SL>(tid, b, r);
-      if (j >= 1 && j < RL) {
-        const double2 x = w[b * RLAST + r];
-        col[(size_t)j * cs] =
-            make_double2((x.x * (1.0 / M2) + cst.x) * s, (x.y * (1.0 / M2) + cst.y) * s);
-      }
+
+  // the K-1 interface values, one lane per mode
+  if (k == 0) {
+    const double A = a.tA[mm];
+    const double* iq = a.tiq + (size_t)mm * K;  // 1 / q_k at [k - 1]
+    double2 z = make_double2(0.0, 0.0);
+    for (int kk = 1; kk < K; ++kk) {
+      double2 r = csub(rint[kk][mi], cadd(lst[kk - 1][mi], fst[kk][mi]));
+      if (kk == 1) r = csub(r, cscale(sp, A));
+      if (kk == K - 1) r = csub(r, cscale(sq, A));
+      z = kk == 1 ? r : csub(r, cscale(z, A * iq[kk - 2]));
+      V[kk][mi] = z;
     }
-  if (tid == 0) col[0] = make_double2((sp.x + cst.x) * s, (sp.y + cst.y) * s);
+    double2 v = cscale(V[K - 1][mi], iq[K - 2]);
+    V[K - 1][mi] = v;
+    for (int kk = K - 2; kk >= 1; --kk) {
+      v = cscale(csub(V[kk][mi], cscale(v, A)), iq[kk - 1]);
+      V[kk][mi] = v;
+    }
+    V[0][mi] = sp;
+    V[K][mi] = sq;
+  }
+  __syncthreads();
+
+  if (!act) return;
+  const double s = a.out_scale;
+  const double2 v0 = V[k][mi], v1 = V[k + 1][mi];
+  const double* g = sg[mi];
+  tile[(size_t)(k * C) << 3] = make_double2((v0.x + cst.x) * s, (v0.y + cst.y) * s);
+#pragma unroll
+  for (int i = 1; i < C; ++i) {
+    const double2 p = cadd(y[i - 1], cadd(cscale(v0, g[i]), cscale(v1, g[C - i])));
+    tile[(size_t)(k * C + i) << 3] = make_double2((p.x + cst.x) * s, (p.y + cst.y) * s);
+  }
 }
 
 __global__ __launch_bounds__(256) void packed_divide_kernel(const PackedDivParams p) {
@@ -217,18 +228,20 @@ __global__ __launch_bounds__(256) void packed_divide_kernel(const PackedDivParam
   if (kp != k) p.Z[kp] = op;
 }
 
-template <int M2>
+template <int K>
 void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
-  const dim3 grid(a.L - 1), block(Plan<M2>::T);
   if (pass == 0)
     hipLaunchKernelGGL(schur_trace_kernel, dim3(a.L / 8), dim3(kTraceThreads), 0, st, a);
   else
-    hipLaunchKernelGGL(schur_solve_kernel<M2>, grid, block, 0, st, a);
+  {
+    constexpr int MW = K >= 128 ? 4 : 8;
+    hipLaunchKernelGGL((schur_solve_kernel<K, MW>), dim3(a.L / MW), dim3(MW * K), 0, st, a);
+  }
 }
 
 }  // namespace
 
-// Slab heights whose odd extension (2 rl) is one of the in-LDS FFT lengths.
+// Slab heights of 16 .. 128 chunks (one workgroup of 8 K <= 1024 threads per tile).
 bool schur_supported(int rl) { return rl == 512 || rl == 1024 || rl == 2048 || rl == 4096; }
 
 void launch_schur_pass(int pass, const SchurArgs& a, hipStream_t st) {
@@ -236,10 +249,10 @@ void launch_schur_pass(int pass, const SchurArgs& a, hipStream_t st) {
       a.rank < 0 || a.rank >= a.P)
     throw Error{CFDJ_ERR_ARG, "substructured Poisson: unsupported slab"};
   switch (a.rl) {
-    case 512: launch_schur_n<1024>(pass, a, st); break;
-    case 1024: launch_schur_n<2048>(pass, a, st); break;
-    case 2048: launch_schur_n<4096>(pass, a, st); break;
-    case 4096: launch_schur_n<8192>(pass, a, st); break;
+    case 512: launch_schur_n<512 / kChunk>(pass, a, st); break;
+    case 1024: launch_schur_n<1024 / kChunk>(pass, a, st); break;
+    case 2048: launch_schur_n<2048 / kChunk>(pass, a, st); break;
+    case 4096: launch_schur_n<4096 / kChunk>(pass, a, st); break;
   }
   CFDJ_HIP(hipGetLastError());
 }
