@@ -50,7 +50,7 @@ extern "C" {
                                  ny 1024..8192, power-of-two rank counts (on y-slabs:
                                  all-to-all transposes of the half spectrum) */
 #define CFDJ_POISSON_SCHUR 3  /* y-slabs only: hand-written row FFTs + substructured y-solve
-                                 (DST-I interiors, P x P separator system; two all-gathers
+                                 (chunked tridiagonal interiors, P x P separator system; two all-gathers
                                  of 64 B per x-mode instead of transposes); square
                                  power-of-two grids, 512..4096 rows per rank.  AUTO on
                                  y-slabs picks it where supported. */

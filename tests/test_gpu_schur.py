@@ -1,12 +1,13 @@
 """GPU parity of the substructured y-slab Poisson path (schur.hip, CFDJ_POISSON_SCHUR):
-row FFTs + per-x-mode periodic y-tridiagonal split at one separator row per slab (DST-I
-interiors, P x P circulant separator system), run as P virtual ranks on one GPU and as a
-one-rank RCCL communicator (tests/test_gpu_rccl.py).
+row FFTs + per-x-mode periodic y-tridiagonal split at one separator row per slab (interiors
+solved directly in 32-row Thomas chunks + an interface system on the GPU, by DST-I in the
+CPU restatement; P x P circulant separator system), run as P virtual ranks on one GPU and
+as a one-rank RCCL communicator (tests/test_gpu_rccl.py).
 
 Tolerances.  The reference (vm_oracle.fps, Common.jl:97-125) divides by D = (aa + bb cos kx)
 + cc cos ky evaluated in double; with |cc| = 2/dy^2 ~ n^2 that rounding perturbs its low
 modes by ~eps * cc / |D|.  The decomposition inverts the same operator through sums of the
-same magnitude (separator system, DST eigenvalues), so two correct implementations agree to
+same magnitude (separator system, interior pivots / DST eigenvalues), so two correct implementations agree to
 ~eps * n^2 relative, not to a fixed 1e-12: psi within tol = 2e-12 * (n/1024)^2 * max|psi|
 of the CPU restatement (oracle/schur_oracle.py) and 2 tol of the reference (the CPU
 restatement itself is 1.2e-12 / 6e-12 from the reference at 1024^2 / 4096^2).  The north-star criterion -- vorticity
