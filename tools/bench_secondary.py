@@ -4,6 +4,11 @@
       3-pass path) vs the CPU oracle (scipy.fft, all host cores), with the MMS L2 error.
   C4  lid-driven cavity (18/lid_driven_cavity.jl) 2048^2, re = 100, dt = 5e-6: ms per RK3
       step with the DST-I (fused FFT on the 4096^2 odd extension) and the V-cycle MG solver.
+  S   spectral solvers (20/hybrid.jl, 21/22 pseudospectral) at 1024^2 and 4096^2: ms per
+      RK3-CN step (rocFFT c2c + elementwise kernels), MLUPS.
+  Y   the multi-GPU y-slab code on one GPU (--virtual P): per-rank ms per step at the
+      weak-scaling grids, i.e. the compute of one rank of an N-GPU run without the RCCL
+      latency (8192^2 / P = 2, 4; 16384^2 / P = 8).
 
   python tools/bench_secondary.py [--steps 20]
 """
@@ -70,9 +75,64 @@ def bench_cavity(n=2048, steps=20, dt=5e-6):
     return out
 
 
+def bench_spectral(steps=5):
+    import math
+
+    from cfd_julia_amd.spectral import SpectralNS2D
+    from cfd_julia_amd.common import vm_ic
+
+    out = []
+    for n in (1024, 4096):
+        dx = 2 * math.pi / n
+        x = dx * np.arange(n + 1)
+        wn = np.zeros((n + 2, n + 2), order="F")
+        vm_ic(n, n, x, x, wn)
+        for kind in ("hybrid", "2/3", "3/2"):
+            with SpectralNS2D(n, n, dx, dx, 1000.0, kind) as h:
+                h.upload(wn)
+                h.step(1e-4, 1)
+                t0 = time.perf_counter()
+                h.step(1e-4, steps)
+                t = time.perf_counter() - t0
+            out.append({"config": f"S {kind} {n}^2", "ms_per_step": round(t * 1e3 / steps, 3),
+                        "MLUPS": round(n * n * steps / t / 1e6, 1)})
+    return out
+
+
+def bench_slabs(steps=3):
+    import math
+
+    from cfd_julia_amd import VortexMerger
+    from cfd_julia_amd.common import vm_ic
+
+    out = []
+    for n, P in ((8192, 2), (8192, 4), (16384, 8)):
+        dx = 2 * math.pi / n
+        dt = 5e-4 * 2.0 * 4096.0 ** 2 / (2 * n * n)
+        with VortexMerger(n, n, dx, dx, 1000.0, kind="virtual", nranks=P) as h:
+            x = dx * np.arange(n + 1)
+            wn = np.zeros((n + 2, n + 2), order="F")
+            vm_ic(n, n, x, x, wn)
+            h.upload(wn)
+            del wn
+            h.step(dt, 1)
+            t0 = time.perf_counter()
+            h.step(dt, steps)
+            t = time.perf_counter() - t0
+            out.append({"config": f"Y {n}^2 virtual {P} slabs ({h.poisson()})",
+                        "ms_per_step_all_slabs": round(t * 1e3 / steps, 3),
+                        "ms_per_step_per_rank": round(t * 1e3 / steps / P, 3),
+                        "cells_per_rank": n * n // P})
+    return out
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
     a = ap.parse_args()
     print(json.dumps(bench_poisson()))
     print(json.dumps(bench_cavity(steps=a.steps)))
+    for r in bench_spectral():
+        print(json.dumps(r))
+    for r in bench_slabs():
+        print(json.dumps(r))
