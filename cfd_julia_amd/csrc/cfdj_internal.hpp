@@ -185,6 +185,7 @@ struct SchurArgs {
   const double* tip;    // [L][32] inverse pivots of a 31-row chunk (system scaled by dy^2)
   const double* tg;     // [L][33] chunk homogeneous solution g(i), g(0) = 1, g(32) = 0
   const double* tA;     // [L] interface off-diagonal g(31)
+  const double* tB;     // [L] interface diagonal -(2 + eps) + 2 g(1)
   const double* tiq;    // [L][K] inverse pivots of the K-1 interface system
   double inv_dy2, dy2, out_scale, inv_ny;
   int rl, L, P, rank;

@@ -301,7 +301,7 @@ struct SchurTables {
   int rl = 0, L = 0, P = 0, K = 0;
   double inv_dy2 = 0, dy2 = 0;
   double *cinv = nullptr, *corr = nullptr, *g = nullptr;
-  double *tip = nullptr, *tg = nullptr, *tA = nullptr, *tiq = nullptr;
+  double *tip = nullptr, *tg = nullptr, *tA = nullptr, *tB = nullptr, *tiq = nullptr;
   bool ready() const { return cinv != nullptr; }
   void init(int nx, int ny, double dx, double dy, double eps, int nranks) {
     typedef long double ld;
@@ -319,7 +319,7 @@ struct SchurTables {
     const double ce = std::cos(kx[0]);  // reference cos(ky[1]) = cos(eps)
     std::vector<double> hc((size_t)L * P, 0.0), hr(L, 0.0);
     std::vector<double> hg((size_t)L * (rl + 1), 0.0);
-    std::vector<double> hip((size_t)L * kC, 0.0), htg((size_t)L * (kC + 1), 0.0), hA(L, 0.0),
+    std::vector<double> hip((size_t)L * kC, 0.0), htg((size_t)L * (kC + 1), 0.0), hA(L, 0.0), hB(L, 1.0),
         hiq((size_t)L * K, 0.0);
     std::vector<ld> s2(rl), qk(rl + 1);
     for (int k = 0; k <= rl; ++k) {
@@ -378,6 +378,7 @@ struct SchurTables {
       // interface system A v_{k-1} + B v_k + A v_{k+1}: A = g(C-1), B = -(2 + ep) + 2 g(1)
       const ld A = gc[kC - 1], B = -(2.0L + ep) + 2.0L * gc[1];
       hA[m] = (double)A;
+      hB[m] = (double)B;
       ld q = B;
       for (int k = 1; k < K; ++k) {
         if (k > 1) q = B - A * A / q;
@@ -390,6 +391,7 @@ struct SchurTables {
     tip = upload(hip);
     tg = upload(htg);
     tA = upload(hA);
+    tB = upload(hB);
     tiq = upload(hiq);
   }
   static double* upload(const std::vector<double>& h) {
@@ -398,7 +400,7 @@ struct SchurTables {
     return d;
   }
   void destroy() {
-    for (double** p : {&cinv, &corr, &g, &tip, &tg, &tA, &tiq}) dfree(*p);
+    for (double** p : {&cinv, &corr, &g, &tip, &tg, &tA, &tB, &tiq}) dfree(*p);
   }
   SchurArgs args(double2* H, double2* T, int rank, double out_scale, int ny) const {
     SchurArgs a;
@@ -410,6 +412,7 @@ struct SchurTables {
     a.tip = tip;
     a.tg = tg;
     a.tA = tA;
+    a.tB = tB;
     a.tiq = tiq;
     a.inv_dy2 = inv_dy2;
     a.dy2 = dy2;

@@ -166,26 +166,55 @@ __global__ __launch_bounds__(MW * K) void schur_solve_kernel(const SchurArgs a) 
   rint[k][mi] = fint;
   __syncthreads();
 
-  // the K-1 interface values, one lane per mode
-  if (k == 0) {
-    const double A = a.tA[mm];
-    const double* iq = a.tiq + (size_t)mm * K;  // 1 / q_k at [k - 1]
-    double2 z = make_double2(0.0, 0.0);
-    for (int kk = 1; kk < K; ++kk) {
-      double2 r = csub(rint[kk][mi], cadd(lst[kk - 1][mi], fst[kk][mi]));
-      if (kk == 1) r = csub(r, cscale(sp, A));
-      if (kk == K - 1) r = csub(r, cscale(sq, A));
-      z = kk == 1 ? r : csub(r, cscale(z, A * iq[kk - 2]));
-      V[kk][mi] = z;
+  // the K-1 interface values by parallel cyclic reduction, lane (mi, k) owning v_k:
+  // a v_{k-s} + b v_k + c v_{k+s} = r, starting from (A, B, A) with v_0 = s_p and v_K = s_q
+  // folded into r; every step eliminates the couplings at distance s (log2 K steps).
+  // Lanes k = 0 carry the identity row.
+  __shared__ double sa[K][MW], sb[K][MW], sc2[K][MW];
+  {
+    const double A = a.tA[mm], B = a.tB[mm];
+    double ca = 0.0, cb = 1.0, cc = 0.0;
+    double2 r = make_double2(0.0, 0.0);
+    if (k >= 1) {
+      ca = k == 1 ? 0.0 : A;
+      cb = B;
+      cc = k == K - 1 ? 0.0 : A;
+      r = csub(rint[k][mi], cadd(lst[k - 1][mi], fst[k][mi]));
+      if (k == 1) r = csub(r, cscale(sp, A));
+      if (k == K - 1) r = csub(r, cscale(sq, A));
     }
-    double2 v = cscale(V[K - 1][mi], iq[K - 2]);
-    V[K - 1][mi] = v;
-    for (int kk = K - 2; kk >= 1; --kk) {
-      v = cscale(csub(V[kk][mi], cscale(v, A)), iq[kk - 1]);
-      V[kk][mi] = v;
+#pragma unroll 1
+    for (int st = 1; st < K; st <<= 1) {
+      sa[k][mi] = ca;
+      sb[k][mi] = cb;
+      sc2[k][mi] = cc;
+      V[k][mi] = r;
+      __syncthreads();
+      const int lo = k - st, hi = k + st;
+      double al = 0.0, ga = 0.0, alo = 0.0, clo = 0.0, ahi = 0.0, chi = 0.0;
+      double2 rlo = make_double2(0.0, 0.0), rhi = rlo;
+      if (k >= 1 && lo >= 1) {
+        al = -ca / sb[lo][mi];
+        alo = sa[lo][mi];
+        clo = sc2[lo][mi];
+        rlo = V[lo][mi];
+      }
+      if (k >= 1 && hi <= K - 1) {
+        ga = -cc / sb[hi][mi];
+        ahi = sa[hi][mi];
+        chi = sc2[hi][mi];
+        rhi = V[hi][mi];
+      }
+      __syncthreads();
+      if (k >= 1) {
+        cb = cb + al * clo + ga * ahi;
+        ca = al * alo;
+        cc = ga * chi;
+        r = cadd(r, cadd(cscale(rlo, al), cscale(rhi, ga)));
+      }
     }
-    V[0][mi] = sp;
-    V[K][mi] = sq;
+    V[k][mi] = k >= 1 ? make_double2(r.x / cb, r.y / cb) : sp;
+    if (k == 0) V[K][mi] = sq;
   }
   __syncthreads();
 
