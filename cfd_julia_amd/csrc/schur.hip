@@ -263,7 +263,13 @@ void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(schur_trace_kernel, dim3(a.L / 8), dim3(kTraceThreads), 0, st, a);
   else
   {
-    constexpr int MW = K >= 128 ? 4 : 8;
+#ifndef CFDJ_SCHUR_MW64
+#define CFDJ_SCHUR_MW64 4
+#endif
+#ifndef CFDJ_SCHUR_MW128
+#define CFDJ_SCHUR_MW128 4
+#endif
+    constexpr int MW = K >= 128 ? CFDJ_SCHUR_MW128 : (K >= 64 ? CFDJ_SCHUR_MW64 : 8);
     hipLaunchKernelGGL((schur_solve_kernel<K, MW>), dim3(a.L / MW), dim3(MW * K), 0, st, a);
   }
 }
