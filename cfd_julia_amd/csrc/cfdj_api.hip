@@ -106,6 +106,12 @@ struct cfdj_vm {
   double2* G = nullptr;
   rocfft_plan g_fwd = nullptr, g_inv = nullptr;
   ncclComm_t comm = nullptr;
+  // RCCL slabs: halo exchanges on a side stream, overlapped with the Poisson passes (omega
+  // halo) and the interior rows of the stage kernel (psi halo).  Collectives stay strictly
+  // ordered: the main stream waits for the omega halo before its first collective.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_src = nullptr, ev_whalo = nullptr, ev_psi = nullptr, ev_shalo = nullptr;
+  bool whalo_pending = false;
   double* gather = nullptr;                                      // Rccl download buffer
   // timing
   bool timing = false;
@@ -158,6 +164,15 @@ struct cfdj_vm {
   }
 
   // ---- communication (slab mode) ------------------------------------------------------
+  // Before a collective on the main stream: the side stream's omega halo (same
+  // communicator) must have completed, so at most one RCCL operation is ever in flight.
+  void comm_order() {
+    if (whalo_pending) {
+      CFDJ_HIP(hipStreamWaitEvent(stream, ev_whalo, 0));
+      whalo_pending = false;
+    }
+  }
+
   // All-to-all of `count` complex elements per peer: send chunk q of slab p -> recv chunk
   // p of slab q.  pick(slab, send?) selects the buffers.
   template <class Pick>
@@ -165,6 +180,7 @@ struct cfdj_vm {
     tbegin(CFDJ_K_COMM);
     if (mode == Mode::Rccl) {
       Slab& s = slabs[0];
+      comm_order();
       CFDJ_NCCL(ncclAllToAll(pick(s, true), pick(s, false), 2 * count, ncclDouble, comm,
                              stream));
     } else {
@@ -180,7 +196,8 @@ struct cfdj_vm {
 
   // Fill the lo/hi ghost rows (offset 0/1 for w, 2/3 for psi) of every slab from the
   // neighbouring slabs' last/first rows.
-  void halo(bool psi_field, const std::vector<const double*>& src) {
+  void halo(bool psi_field, const std::vector<const double*>& src) { halo(psi_field, src, stream); }
+  void halo(bool psi_field, const std::vector<const double*>& src, hipStream_t hs) {
     const int off = psi_field ? 2 : 0;
     const size_t bytes = (size_t)nx * sizeof(double);
     tbegin(CFDJ_K_COMM);
@@ -194,10 +211,10 @@ struct cfdj_vm {
       // Order matters when prev == next (2 ranks): sends [to prev, to next], receives
       // [from next, from prev] so the k-th message between a pair matches by role.
       CFDJ_NCCL(ncclGroupStart());
-      CFDJ_NCCL(ncclSend(first, nx, ncclDouble, prev, comm, stream));
-      CFDJ_NCCL(ncclSend(last, nx, ncclDouble, next, comm, stream));
-      CFDJ_NCCL(ncclRecv(hi, nx, ncclDouble, next, comm, stream));
-      CFDJ_NCCL(ncclRecv(lo, nx, ncclDouble, prev, comm, stream));
+      CFDJ_NCCL(ncclSend(first, nx, ncclDouble, prev, comm, hs));
+      CFDJ_NCCL(ncclSend(last, nx, ncclDouble, next, comm, hs));
+      CFDJ_NCCL(ncclRecv(hi, nx, ncclDouble, next, comm, hs));
+      CFDJ_NCCL(ncclRecv(lo, nx, ncclDouble, prev, comm, hs));
       CFDJ_NCCL(ncclGroupEnd());
     } else {
       const int P = (int)slabs.size();
@@ -331,8 +348,10 @@ struct cfdj_vm {
     for (auto& s : slabs)
       CFDJ_HIP(hipMemcpy2DAsync(G + s.row0, sizeof(double2), s.X, 8 * sizeof(double2),
                                 sizeof(double2), rows, hipMemcpyDeviceToDevice, stream));
-    if (mode == Mode::Rccl)
+    if (mode == Mode::Rccl) {
+      comm_order();
       CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, stream));
+    }
     tend();
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
@@ -399,6 +418,8 @@ struct cfdj_vm {
     p.out = out;
     p.nx = nx;
     p.ny = rows;
+    p.y0 = 0;
+    p.ycount = rows;
     p.rows_per_wave = rows_per_wave;
     const double dx2 = dx * dx, dy2 = dy * dy;
     p.k.aa = 1.0 / (re * dx2);
@@ -418,6 +439,10 @@ struct cfdj_vm {
     std::vector<const double*> src(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i)
       src[i] = st == 1 ? slabs[i].wn : st == 2 ? slabs[i].wa : slabs[i].wb;
+    if (mode == Mode::Rccl && side && !timing && rows >= 4) {
+      stage_overlapped(st, dt, src[0]);
+      return;
+    }
     poisson(src, true);
     if (slab_mode()) {
       halo(false, src);
@@ -432,6 +457,35 @@ struct cfdj_vm {
       launch_stage(st, stage_params(s, src[i], s.wn, out, dt), stream);
       tend();
     }
+  }
+
+  // The RCCL-slab stage with the halo exchanges on the side stream: omega halo during the
+  // Poisson passes, psi halo during the interior rows of the stage kernel; the first and
+  // last rows (which read the halo rows) run after it.
+  void stage_overlapped(int st, double dt, const double* src) {
+    Slab& s = slabs[0];
+    CFDJ_HIP(hipEventRecord(ev_src, stream));
+    CFDJ_HIP(hipStreamWaitEvent(side, ev_src, 0));
+    halo(false, {src}, side);
+    CFDJ_HIP(hipEventRecord(ev_whalo, side));
+    whalo_pending = true;
+    poisson({src}, true);
+    comm_order();  // paths without a collective before the psi halo
+    CFDJ_HIP(hipEventRecord(ev_psi, stream));
+    CFDJ_HIP(hipStreamWaitEvent(side, ev_psi, 0));
+    halo(true, {s.psi}, side);
+    CFDJ_HIP(hipEventRecord(ev_shalo, side));
+    double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
+    StageParams p = stage_params(s, src, s.wn, out, dt);
+    p.y0 = 1;
+    p.ycount = rows - 2;
+    launch_stage(st, p, stream);
+    CFDJ_HIP(hipStreamWaitEvent(stream, ev_shalo, 0));
+    p.ycount = 1;
+    p.y0 = 0;
+    launch_stage(st, p, stream);
+    p.y0 = rows - 1;
+    launch_stage(st, p, stream);
   }
 
   // `n` back-to-back launches of ONE kernel of the step between two events on the handle's
@@ -584,6 +638,7 @@ struct cfdj_vm {
   }
 
   void sync() {
+    if (side) CFDJ_HIP(hipStreamSynchronize(side));
     CFDJ_HIP(hipStreamSynchronize(stream));
     harvest();
     if (check_finite) {
@@ -679,6 +734,10 @@ struct cfdj_vm {
     dfree(gather);
     dfree(d_flag);
     for (auto e : ev) (void)hipEventDestroy(e);
+    if (side) (void)hipStreamSynchronize(side);
+    for (hipEvent_t e : {ev_src, ev_whalo, ev_psi, ev_shalo})
+      if (e) (void)hipEventDestroy(e);
+    if (side) (void)hipStreamDestroy(side);
     if (comm) ncclCommDestroy(comm);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -889,6 +948,13 @@ int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double 
     ncclUniqueId id;
     std::memcpy(&id, nccl_id, sizeof(id));
     CFDJ_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
+    // halo overlap (CFDJ_NO_OVERLAP=1: everything on one stream, for A/B runs)
+    const char* no_ov = std::getenv("CFDJ_NO_OVERLAP");
+    if (!(no_ov && no_ov[0] == '1')) {
+      CFDJ_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
+      for (hipEvent_t* e : {&h->ev_src, &h->ev_whalo, &h->ev_psi, &h->ev_shalo})
+        CFDJ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    }
     *out = h.release();
   });
 }

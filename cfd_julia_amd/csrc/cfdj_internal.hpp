@@ -84,6 +84,7 @@ struct StageParams {
   const double* wn;    // omega^n (pointwise; stages 2 and 3)
   double* out;         // stage output (stage 0: the bare RHS r)
   int nx, ny;
+  int y0, ycount;      // rows [y0, y0 + ycount) of the slab are computed (halo split)
   int rows_per_wave;
   StageCoef k;
 };

@@ -45,9 +45,10 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
   const int xl = xs == 0 ? nx - 1 : xs - 1;
   const int xr = xs + 2 >= nx ? xs + 2 - nx : xs + 2;
 
-  const int ybeg = (chunk * kWavesPerBlock + wave) * p.rows_per_wave;
-  if (ybeg >= ny) return;
-  const int yend = min(ybeg + p.rows_per_wave, ny);
+  const int ylim = p.y0 + p.ycount;
+  const int ybeg = p.y0 + (chunk * kWavesPerBlock + wave) * p.rows_per_wave;
+  if (ybeg >= ylim) return;
+  const int yend = min(ybeg + p.rows_per_wave, ylim);
 
   const StageCoef k = p.k;
   Raw wr_p = fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg + 1, ny, nx), xs, xl, xr, is_l, is_r);
@@ -160,7 +161,9 @@ __global__ __launch_bounds__(256) void finite_kernel(const double* __restrict__ 
 void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   const int rpw = p.rows_per_wave;
   const long strips = (p.nx + kColsPerWave - 1) / kColsPerWave;
-  const long chunks = (p.ny + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw);
+  if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
+    throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};
+  const long chunks = (p.ycount + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw);
   if (strips * chunks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
   dim3 grid((unsigned)(strips * chunks));
   dim3 block(kWave * kWavesPerBlock);
