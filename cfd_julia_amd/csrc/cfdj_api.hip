@@ -66,6 +66,13 @@ struct Slab {
   double *wn = nullptr, *wa = nullptr, *wb = nullptr, *psi = nullptr;
   double* ghost = nullptr;  // 4 rows: w_lo, w_hi, s_lo, s_hi (slab mode only)
   double2 *X = nullptr, *S = nullptr, *Y = nullptr;  // slab-FFT buffers
+  // Schur path: column-sum partials of wn / wa / wb as the stage kernel writes them
+  // ([rows / rows_per_wave][nx], valid once a stage kernel or colpart wrote them), the
+  // column-sum row padded to 8 rows (cs8) and its tiled row spectrum (cs)
+  double* colpart[4] = {nullptr, nullptr, nullptr, nullptr};  // [3]: other inputs
+  bool cp_valid[3] = {false, false, false};
+  double* cs8 = nullptr;
+  double2* cs = nullptr;
   void destroy() {
     dfree(wn);
     dfree(wa);
@@ -75,6 +82,9 @@ struct Slab {
     dfree(X);
     dfree(S);
     dfree(Y);
+    for (auto& c : colpart) dfree(c);
+    dfree(cs8);
+    dfree(cs);
   }
 };
 
@@ -103,6 +113,7 @@ struct cfdj_vm {
   SchurTables schur;
   bool use_schur = false;
   double2* T = nullptr;
+  int ncp = 0;  // column-sum partial rows (blocks of rows_per_wave rows)
   double2* G = nullptr;
   rocfft_plan g_fwd = nullptr, g_inv = nullptr;
   ncclComm_t comm = nullptr;
@@ -161,6 +172,19 @@ struct cfdj_vm {
     }
     ev_used = 0;
     ev_cat.clear();
+  }
+
+  // Column-sum partial buffers of the Schur path, one block per rows_per_wave rows (the
+  // stage kernel's wave row ranges); re-sized and invalidated when rows_per_wave changes.
+  void alloc_colparts() {
+    ncp = (rows + rows_per_wave - 1) / rows_per_wave;
+    for (auto& s : slabs) {
+      for (auto& c : s.colpart) {
+        dfree(c);
+        c = dalloc<double>((size_t)ncp * nx);
+      }
+      for (bool& v : s.cp_valid) v = false;
+    }
   }
 
   // ---- communication (slab mode) ------------------------------------------------------
@@ -330,8 +354,25 @@ struct cfdj_vm {
     auto schur_args = [&](const Slab& s) {
       SchurArgs sa = schur.args(s.X, T, s.rank, out_scale, ny);
       sa.tile8 = 1;
+      sa.cs = s.cs;
       return sa;
     };
+    // the slab's column sum per mode: the stage kernel's partials of this input (or a
+    // colpart pass for other inputs), summed to one row, row r2c -> cs (8-mode tiles)
+    for (size_t i = 0; i < slabs.size(); ++i) {
+      Slab& s = slabs[i];
+      const int idx = src[i] == s.wn ? 0 : src[i] == s.wa ? 1 : src[i] == s.wb ? 2 : 3;
+      tbegin(CFDJ_K_FFT_FWD);
+      if (idx == 3 || !s.cp_valid[idx]) {
+        launch_colpart(src[i], nx, rows, rows_per_wave, s.colpart[idx], stream);
+        if (idx < 3) s.cp_valid[idx] = true;
+      }
+      launch_colsum_row(s.colpart[idx], ncp, nx, s.cs8, stream);
+      FusedPoissonArgs ca = fused.args(sym, s.cs8, nullptr, s.cs, s.cs, 8, 0, 1, neg);
+      ca.tile8 = 1;
+      launch_fused_poisson_pass(0, ca, stream);
+      tend();
+    }
     std::vector<FusedPoissonArgs> a;
     for (size_t i = 0; i < slabs.size(); ++i) {
       a.push_back(fused.args(sym, src[i], slabs[i].psi, slabs[i].X, slabs[i].X, rows,
@@ -420,6 +461,7 @@ struct cfdj_vm {
     p.ny = rows;
     p.y0 = 0;
     p.ycount = rows;
+    p.colpart = nullptr;
     p.rows_per_wave = rows_per_wave;
     const double dx2 = dx * dx, dy2 = dy * dy;
     p.k.aa = 1.0 / (re * dx2);
@@ -439,7 +481,8 @@ struct cfdj_vm {
     std::vector<const double*> src(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i)
       src[i] = st == 1 ? slabs[i].wn : st == 2 ? slabs[i].wa : slabs[i].wb;
-    if (mode == Mode::Rccl && side && !timing && rows >= 4) {
+    if (mode == Mode::Rccl && side && !timing && rows % rows_per_wave == 0 &&
+        rows >= 3 * rows_per_wave) {
       stage_overlapped(st, dt, src[0]);
       return;
     }
@@ -454,7 +497,13 @@ struct cfdj_vm {
       Slab& s = slabs[i];
       double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
       tbegin(CFDJ_K_STAGE);
-      launch_stage(st, stage_params(s, src[i], s.wn, out, dt), stream);
+      StageParams p = stage_params(s, src[i], s.wn, out, dt);
+      if (use_schur) {  // column-sum partials of the output for the next stage's Poisson
+        const int oi = st == 1 ? 1 : st == 2 ? 2 : 0;
+        p.colpart = s.colpart[oi];
+        s.cp_valid[oi] = true;
+      }
+      launch_stage(st, p, stream);
       tend();
     }
   }
@@ -477,14 +526,22 @@ struct cfdj_vm {
     CFDJ_HIP(hipEventRecord(ev_shalo, side));
     double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
     StageParams p = stage_params(s, src, s.wn, out, dt);
-    p.y0 = 1;
-    p.ycount = rows - 2;
+    if (use_schur) {
+      const int oi = st == 1 ? 1 : st == 2 ? 2 : 0;
+      p.colpart = s.colpart[oi];
+      s.cp_valid[oi] = true;
+    }
+    // interior blocks first, then the first / last rows_per_wave rows (which read the halo
+    // rows); block-aligned, so the column partials match the one-launch order
+    const int rb = rows_per_wave;
+    p.y0 = rb;
+    p.ycount = rows - 2 * rb;
     launch_stage(st, p, stream);
     CFDJ_HIP(hipStreamWaitEvent(stream, ev_shalo, 0));
-    p.ycount = 1;
+    p.ycount = rb;
     p.y0 = 0;
     launch_stage(st, p, stream);
-    p.y0 = rows - 1;
+    p.y0 = rows - rb;
     launch_stage(st, p, stream);
   }
 
@@ -609,6 +666,8 @@ struct cfdj_vm {
 
   void step_async(double dt, int nsteps) {
     if (nsteps == 0) return;
+    // omega^n may have changed since the last step (upload, cfdj_vm_field_device users)
+    for (auto& s : slabs) s.cp_valid[0] = false;
     // Graphs only around our own kernels (rocFFT calls are not captured), and never with
     // timing on: event-record nodes captured from hipEventRecord are not recorded on this
     // ROCm (hipEventElapsedTime -> invalid resource handle), so timed runs launch eagerly.
@@ -713,6 +772,13 @@ struct cfdj_vm {
       use_fused = true;
     }
     if (use_schur && !fused.ready()) fused.init(nx, ny);  // row-pass twiddles
+    if (use_schur) {
+      for (auto& s : slabs) {
+        s.cs8 = dalloc<double>((size_t)8 * nx);
+        s.cs = dalloc<double2>((size_t)8 * (nx / 2));
+      }
+      alloc_colparts();
+    }
     // second row spectrum of the FFT-fused stage (allocated up front: never inside a
     // graph capture)
     if (mode == Mode::Single && fused_stage_supported(nx, ny))
@@ -1037,6 +1103,7 @@ int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, doub
     const size_t rowb = nx * sizeof(double);
     std::vector<const double*> src;
     for (auto& sl : h->slabs) {
+      sl.cp_valid[1] = sl.cp_valid[2] = false;  // wa / wb are scratch here
       CFDJ_HIP(hipMemcpy2DAsync(sl.wa, rowb, w + 1 + (size_t)(1 + sl.row0) * ldw,
                                 ldw * sizeof(double), rowb, sl.rows, hipMemcpyHostToDevice,
                                 h->stream));
@@ -1125,7 +1192,10 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
   return guard([&] {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
     CFDJ_REQUIRE(rows >= 1, "rows must be >= 1");
+    select_device(h->device);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
     h->rows_per_wave = rows;
+    if (h->use_schur) h->alloc_colparts();  // partial blocks follow the wave row ranges
     h->invalidate_graph();
   });
 }

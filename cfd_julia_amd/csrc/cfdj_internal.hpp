@@ -85,11 +85,18 @@ struct StageParams {
   double* out;         // stage output (stage 0: the bare RHS r)
   int nx, ny;
   int y0, ycount;      // rows [y0, y0 + ycount) of the slab are computed (halo split)
+  double* colpart;     // optional: per-wave column sums of `out`, [y / rows_per_wave][nx]
   int rows_per_wave;
   StageCoef k;
 };
 
 void launch_stage(int stage, const StageParams& p, hipStream_t st);
+// Column sums of a slab field in the stage kernel's partial layout (rows_per_wave blocks):
+// colpart[b][x] = sum of f[y][x] over rows y of block b (fields not written by a stage).
+void launch_colpart(const double* f, int nx, int rows, int rpw, double* colpart,
+                    hipStream_t st);
+// out8[0][x] = sum over the nb blocks of colpart[b][x]; rows 1..7 of out8 zeroed.
+void launch_colsum_row(const double* colpart, int nb, int nx, double* out8, hipStream_t st);
 
 // Spectral divide (Common.jl:118-121) on a (width x rows) block of the half spectrum
 // stored with row pitch `pitch` (complex elements); column i of the block is the
@@ -183,6 +190,9 @@ struct SchurArgs {
   const double* cinv;   // [L][P] first row of the inverse circulant separator system
   const double* corr;   // [L] 1/D_ref(m, 0) - 1/e_m (the reference's ky[1] = eps)
   const double* g;      // trace Green's function gL(j), j = 0..rl, in 8-mode tiles
+  const double2* cs;    // spectrum of the slab's column sum (row 0 of an 8-row tile
+                        // spectrum): the trace's column sum per mode
+  const int* jt;        // [L/8] rows of a tile's traces above round-off (gL decay)
   const double* tip;    // [L][32] inverse pivots of a 31-row chunk (system scaled by dy^2)
   const double* tg;     // [L][33] chunk homogeneous solution g(i), g(0) = 1, g(32) = 0
   const double* tA;     // [L] interface off-diagonal g(31)

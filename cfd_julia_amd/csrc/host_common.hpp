@@ -1,6 +1,7 @@
 // Host-side helpers shared by the libcfdj.so translation units: error guard, device
 // allocation, the Poisson symbol tables, rocFFT plan bundles and the fused-FFT state.
 #pragma once
+#include <algorithm>
 
 #include "cfdj_internal.hpp"
 
@@ -302,6 +303,7 @@ struct SchurTables {
   double inv_dy2 = 0, dy2 = 0;
   double *cinv = nullptr, *corr = nullptr, *g = nullptr;
   double *tip = nullptr, *tg = nullptr, *tA = nullptr, *tB = nullptr, *tiq = nullptr;
+  int* jt = nullptr;  // [L/8] trace rows above round-off per tile
   bool ready() const { return cinv != nullptr; }
   void init(int nx, int ny, double dx, double dy, double eps, int nranks) {
     typedef long double ld;
@@ -321,6 +323,7 @@ struct SchurTables {
     std::vector<double> hg((size_t)L * (rl + 1), 0.0);
     std::vector<double> hip((size_t)L * kC, 0.0), htg((size_t)L * (kC + 1), 0.0), hA(L, 0.0), hB(L, 1.0),
         hiq((size_t)L * K, 0.0);
+    std::vector<int> hjt(L / 8, 1);
     std::vector<ld> s2(rl), qk(rl + 1);
     for (int k = 0; k <= rl; ++k) {
       const ld sn = sinl(pi * (ld)k / (ld)(2 * rl));
@@ -362,6 +365,10 @@ struct SchurTables {
       const ld ep = -em / o;
       const ld x = ep / 2.0L;
       const ld th = log1pl(x + sqrtl(x * (x + 2.0L)));
+      // gL(j) <= e^{-j th}: below 2^-64 of gL(1) beyond j = 45 / th (+2 for safety)
+      const ld jcut = 45.0L / th + 2.0L;
+      const int jm = jcut >= (ld)rl ? rl : (int)jcut;
+      hjt[m >> 3] = std::max(hjt[m >> 3], jm);
       for (int j = 0; j <= rl; ++j)  // trace pass: gL over the slab, 8-mode tiles
         hg[(((size_t)(m >> 3)) * (rl + 1) + j) * 8 + (m & 7)] = (double)homog(th, rl, j);
       // chunk Thomas pivots p_i = -(1 + s_i): s_1 = 1 + ep, s_i = (s(1 + ep) + ep)/(1 + s)
@@ -393,6 +400,8 @@ struct SchurTables {
     tA = upload(hA);
     tB = upload(hB);
     tiq = upload(hiq);
+    jt = dalloc<int>(hjt.size());
+    CFDJ_HIP(hipMemcpy(jt, hjt.data(), hjt.size() * sizeof(int), hipMemcpyHostToDevice));
   }
   static double* upload(const std::vector<double>& h) {
     double* d = dalloc<double>(h.size());
@@ -401,6 +410,7 @@ struct SchurTables {
   }
   void destroy() {
     for (double** p : {&cinv, &corr, &g, &tip, &tg, &tA, &tB, &tiq}) dfree(*p);
+    dfree(jt);
   }
   SchurArgs args(double2* H, double2* T, int rank, double out_scale, int ny) const {
     SchurArgs a;
@@ -413,6 +423,8 @@ struct SchurTables {
     a.tg = tg;
     a.tA = tA;
     a.tB = tB;
+    a.jt = jt;
+    a.cs = nullptr;
     a.tiq = tiq;
     a.inv_dy2 = inv_dy2;
     a.dy2 = dy2;

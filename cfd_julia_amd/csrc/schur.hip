@@ -45,12 +45,23 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
   const int rl = a.rl;
   const double2* tile = a.H + (((size_t)tb * rl) << 3);
   const double* g = a.g + (((size_t)tb * (rl + 1)) << 3) + mi;
-  double2 t1 = make_double2(0.0, 0.0), tn = t1, fs = t1;
-  for (int j = 1 + r0; j < rl; j += kTraceThreads / 8) {
-    const double2 f = tile[((size_t)j << 3) + mi];
-    t1 = cadd(t1, cscale(f, g[(size_t)j << 3]));
-    tn = cadd(tn, cscale(f, g[(size_t)(rl - j) << 3]));
-    fs = cadd(fs, f);
+  // gL decays like e^{-j th_m}: only the first / last jt rows of the tile's modes carry
+  // trace terms above round-off (host-tabulated, jt = rl for the slowest modes); the
+  // column sum comes from the stage kernel's column partials (a.cs), not from this pass
+  double2 t1 = make_double2(0.0, 0.0), tn = t1;
+  const int J = a.jt[tb];
+  constexpr int RS = kTraceThreads / 8;
+  if (2 * J >= rl - 1) {
+    for (int j = 1 + r0; j < rl; j += RS) {
+      const double2 f = tile[((size_t)j << 3) + mi];
+      t1 = cadd(t1, cscale(f, g[(size_t)j << 3]));
+      tn = cadd(tn, cscale(f, g[(size_t)(rl - j) << 3]));
+    }
+  } else {
+    for (int j = 1 + r0; j <= J; j += RS)
+      t1 = cadd(t1, cscale(tile[((size_t)j << 3) + mi], g[(size_t)j << 3]));
+    for (int j = rl - J + r0; j < rl; j += RS)
+      tn = cadd(tn, cscale(tile[((size_t)j << 3) + mi], g[(size_t)(rl - j) << 3]));
   }
   // sum over the 8 row lanes of a wavefront with the same mode, then over the 4 waves
 #pragma unroll
@@ -59,24 +70,20 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
     t1.y += __shfl_xor(t1.y, o);
     tn.x += __shfl_xor(tn.x, o);
     tn.y += __shfl_xor(tn.y, o);
-    fs.x += __shfl_xor(fs.x, o);
-    fs.y += __shfl_xor(fs.y, o);
   }
   constexpr int W = kTraceThreads / 64;
-  __shared__ double2 red[3][W][8];
+  __shared__ double2 red[2][W][8];
   const int wv = threadIdx.x / 64, ln = threadIdx.x % 64;
   if (ln < 8) {
     red[0][wv][ln] = t1;
     red[1][wv][ln] = tn;
-    red[2][wv][ln] = fs;
   }
   __syncthreads();
   if (threadIdx.x < 8 && m >= 1) {
-    t1 = tn = fs = make_double2(0.0, 0.0);
+    t1 = tn = make_double2(0.0, 0.0);
     for (int w = 0; w < W; ++w) {
       t1 = cadd(t1, red[0][w][mi]);
       tn = cadd(tn, red[1][w][mi]);
-      fs = cadd(fs, red[2][w][mi]);
     }
     const double2 fsep = tile[mi];
     const double mdy2 = -1.0 / a.inv_dy2;
@@ -84,7 +91,9 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
     out[0] = fsep;
     out[1] = cscale(t1, mdy2);
     out[2] = cscale(tn, mdy2);
-    out[3] = cadd(fs, fsep);
+    // column sum over all rows of the slab, separator included: the row r2c of the
+    // slab's column-sum row (element (m, 0) of the 8-row tile spectrum a.cs)
+    out[3] = a.cs[((size_t)(m >> 3) << 6) + (m & 7)];
   }
 }
 

@@ -58,6 +58,7 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
   Win wc = expand(fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
   Win sc = expand(fetch(row_ptr(p.s, p.s_lo, p.s_hi, ybeg, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
 
+  double2 csum = make_double2(0.0, 0.0);  // this wave's column sums of `out` (colpart)
   for (int y = ybeg; y < yend; ++y) {
     // prefetch row y+2 (clamped: the last iteration re-reads row yend, harmlessly)
     const int yn = min(y + 2, yend);
@@ -83,6 +84,8 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
 #else
     if (valid) *reinterpret_cast<double2*>(p.out + (size_t)y * nx + xs) = o;
 #endif
+    csum.x += o.x;
+    csum.y += o.y;
 
     wm = wc;
     wc = wp;
@@ -91,6 +94,41 @@ __global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
     wr_p = wr_n;
     sr_p = sr_n;
   }
+  if (p.colpart != nullptr && valid)
+    *reinterpret_cast<double2*>(p.colpart + (size_t)(ybeg / p.rows_per_wave) * nx + xs) = csum;
+}
+
+// colpart[b][x] = sum over rows [b rpw, (b+1) rpw) of f[y][x], in the row order of the
+// stage kernel's csum (so a field gets the same partials either way).
+__global__ __launch_bounds__(256) void colpart_kernel(const double* __restrict__ f, int nx,
+                                                      int rows, int rpw,
+                                                      double* __restrict__ colpart) {
+  const int x = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (x >= nx) return;
+  double s = 0.0;
+  const int y1 = min((b + 1) * rpw, rows);
+  for (int y = b * rpw; y < y1; ++y) s += f[(size_t)y * nx + x];
+  colpart[(size_t)b * nx + x] = s;
+}
+
+// out8[0][x] = sum of the nb partial rows; 64 columns per workgroup, the 4 waves sum every
+// 4th block, then add up in a fixed order; rows 1..7 of out8 zeroed.
+__global__ __launch_bounds__(256) void colsum_row_kernel(const double* __restrict__ colpart,
+                                                         int nb, int nx,
+                                                         double* __restrict__ out8) {
+  __shared__ double part[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int x = blockIdx.x * 64 + lane;
+  double s = 0.0;
+  if (x < nx)
+    for (int b = w; b < nb; b += 4) s += colpart[(size_t)b * nx + x];
+  part[w][lane] = s;
+  __syncthreads();
+  if (x >= nx) return;
+  if (w == 0) out8[x] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  else out8[(size_t)w * nx + x] = 0.0;
+  out8[(size_t)(w + 4) * nx + x] = 0.0;
 }
 
 __global__ __launch_bounds__(256) void divide_kernel(const DivideParams p) {
@@ -173,6 +211,19 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
     case 2: hipLaunchKernelGGL(vm_stage_kernel<2>, grid, block, 0, st, p); break;
     default: hipLaunchKernelGGL(vm_stage_kernel<3>, grid, block, 0, st, p); break;
   }
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_colpart(const double* f, int nx, int rows, int rpw, double* colpart,
+                    hipStream_t st) {
+  const dim3 grid((nx + 255) / 256, (rows + rpw - 1) / rpw);
+  hipLaunchKernelGGL(colpart_kernel, grid, dim3(256), 0, st, f, nx, rows, rpw, colpart);
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_colsum_row(const double* colpart, int nb, int nx, double* out8, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_row_kernel, dim3((nx + 63) / 64), dim3(256), 0, st, colpart, nb,
+                     nx, out8);
   CFDJ_HIP(hipGetLastError());
 }
 
