@@ -7,11 +7,13 @@ from __future__ import annotations
 
 import ctypes as C
 import math
+import os
 
 import numpy as np
 
 from . import _lib
 from ._lib import check, dptr
+from .fieldio import write_field, write_res_plot
 
 
 class Cavity:
@@ -106,8 +108,9 @@ def numerical(nx, ny, nt, dx, dy, dt, re, wn, sn, rms, device=-1, poisson="dst")
     return None
 
 
-def main(nx=64, ny=64, dt=0.001, tf=10.0, re=100.0, poisson="dst"):
-    """lid_driven_cavity.jl:161-216 without the text files: returns (wn, sn, rms)."""
+def main(nx=64, ny=64, dt=0.001, tf=10.0, re=100.0, poisson="dst", outdir=None):
+    """lid_driven_cavity.jl:161-216: returns (wn, sn, rms); with outdir, also writes the
+    reference's res_plot.txt ("n rms") and field_final.txt ("x y ω ψ") there."""
     dx = (1.0 - 0.0) / nx
     dy = (1.0 - 0.0) / ny
     nt = int(tf / dt)
@@ -115,4 +118,9 @@ def main(nx=64, ny=64, dt=0.001, tf=10.0, re=100.0, poisson="dst"):
     sn = np.zeros((nx + 1, ny + 1), order="F")
     rms = np.empty(nt)
     numerical(nx, ny, nt, dx, dy, dt, re, wn, sn, rms, poisson=poisson)
+    if outdir is not None:
+        x = dx * np.arange(nx + 1, dtype=np.float64)
+        y = dy * np.arange(ny + 1, dtype=np.float64)
+        write_res_plot(os.path.join(outdir, "res_plot.txt"), rms)
+        write_field(os.path.join(outdir, "field_final.txt"), x, y, wn, sn)
     return wn, sn, rms

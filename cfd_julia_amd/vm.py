@@ -14,18 +14,14 @@ import os
 import numpy as np
 
 from .common import periodic_ghosts, vm_ic
+from .fieldio import write_field
 from .solver import VortexMerger
 
 
 def _write_field(path, x, y, ut):
-    """vm.jl:81-85 format: "x y ω" per line, j outer / i inner over (nx+1)(ny+1) nodes."""
-    nxp, nyp = ut.shape
-    X = np.broadcast_to(np.asarray(x[:nxp])[:, None], (nxp, nyp))
-    Y = np.broadcast_to(np.asarray(y[:nyp])[None, :], (nxp, nyp))
-    rows = np.stack([X.T.ravel(), Y.T.ravel(), ut.T.ravel()], axis=1)
-    with open(path, "w") as io:
-        for a, b, c in rows.tolist():  # Python floats: shortest round-trip repr
-            io.write(f"{a!r} {b!r} {c!r}\n")
+    """vm.jl:81-85 format: "x y ω" per line, j outer / i inner over (nx+1)(ny+1) nodes,
+    numbers as Julia prints them (fieldio.julia_str)."""
+    write_field(path, x, y, ut)
 
 
 def numerical(nx, ny, nt, dx, dy, dt, re, x, y, wn, ns, *, snapshots=True, outdir=".",

@@ -134,3 +134,19 @@ def test_gpu_jacobi_converges_mms(lib):
     u = np.asfortranarray(un.copy())
     it, rms = gauss_seidel(dx, dy, n, n, None, f, u, 20000, 1e-9, freq=100)
     assert it < 5 * 20000 and np.abs(u - ue).max() < 1e-7
+
+
+# ---- lid_driven_cavity.jl:161-216 main + its text output --------------------------------
+def test_gpu_cavity_main_writes_reference_files(lib, tmp_path):
+    from cfd_julia_amd import cavity
+    from cfd_julia_amd.fieldio import read_field
+
+    n = 32
+    wn, sn, rms = cavity.main(nx=n, ny=n, dt=0.001, tf=0.02, re=100.0, outdir=str(tmp_path))
+    res = np.loadtxt(tmp_path / "res_plot.txt", ndmin=2)
+    assert res.shape == (20, 2) and np.array_equal(res[:, 0], np.arange(1, 21))
+    assert np.array_equal(res[:, 1], rms)
+    assert np.array_equal(read_field(tmp_path / "field_final.txt", n, n, 2), wn)
+    assert np.array_equal(read_field(tmp_path / "field_final.txt", n, n, 3), sn)
+    xy = np.loadtxt(tmp_path / "field_final.txt")[:, :2]
+    assert xy[1, 0] == 1.0 / n and xy[n + 1, 1] == 1.0 / n

@@ -159,6 +159,8 @@ def test_gpu_vm_numerical_reference_signature(cfdj, tmp_path):
     x, y, val = map(float, lines[1].split())
     assert x == c["x"][1] and y == c["y"][0] and val == un[1, 0]
     assert not (tmp_path / "vm2.txt").exists()
+    from cfd_julia_amd.fieldio import read_field
+    assert np.array_equal(read_field(tmp_path / "vm1.txt", 64, 64), un)  # plotting.jl reader
 
 
 def test_gpu_tgv_known_answer(cfdj, golden):
