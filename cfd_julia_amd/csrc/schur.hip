@@ -51,17 +51,37 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
   double2 t1 = make_double2(0.0, 0.0), tn = t1;
   const int J = a.jt[tb];
   constexpr int RS = kTraceThreads / 8;
-  if (2 * J >= rl - 1) {
-    for (int j = 1 + r0; j < rl; j += RS) {
-      const double2 f = tile[((size_t)j << 3) + mi];
-      t1 = cadd(t1, cscale(f, g[(size_t)j << 3]));
-      tn = cadd(tn, cscale(f, g[(size_t)(rl - j) << 3]));
+  // loads in batches of U rows per lane (the lane's rows still summed in increasing j, so
+  // the result does not depend on U): the slowest tiles' full-column loop is load-latency
+  // bound, one batch in flight per iteration
+  constexpr int U = 8;
+  auto sweep = [&](int jb, int je, bool first, bool last) {
+    for (int j0 = jb + r0; j0 < je; j0 += U * RS) {
+      double2 f[U];
+      double g1[U], gn[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = j0 + u * RS;
+        const bool ok = j < je;
+        const int jj = ok ? j : jb;
+        f[u] = ok ? tile[((size_t)jj << 3) + mi] : make_double2(0.0, 0.0);
+        g1[u] = first ? g[(size_t)jj << 3] : 0.0;
+        gn[u] = last ? g[(size_t)(rl - jj) << 3] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (j0 + u * RS < je) {
+          if (first) t1 = cadd(t1, cscale(f[u], g1[u]));
+          if (last) tn = cadd(tn, cscale(f[u], gn[u]));
+        }
+      }
     }
+  };
+  if (2 * J >= rl - 1) {
+    sweep(1, rl, true, true);
   } else {
-    for (int j = 1 + r0; j <= J; j += RS)
-      t1 = cadd(t1, cscale(tile[((size_t)j << 3) + mi], g[(size_t)j << 3]));
-    for (int j = rl - J + r0; j < rl; j += RS)
-      tn = cadd(tn, cscale(tile[((size_t)j << 3) + mi], g[(size_t)(rl - j) << 3]));
+    sweep(1, J + 1, true, false);
+    sweep(rl - J, rl, false, true);
   }
   // sum over the 8 row lanes of a wavefront with the same mode, then over the 4 waves
 #pragma unroll
