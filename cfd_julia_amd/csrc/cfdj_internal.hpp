@@ -11,6 +11,11 @@
 
 #include "cfdj.h"
 
+// rows per chunk of the Schur interior solve (schur.hip, host_common.hpp SchurTables)
+#ifndef CFDJ_SCHUR_CHUNK
+#define CFDJ_SCHUR_CHUNK 32
+#endif
+
 namespace cfdj {
 
 // ---- errors ------------------------------------------------------------------------

@@ -298,7 +298,7 @@ struct Fused {
 
 // Tables of the substructured y-slab solve (schur.hip), built in long double.
 struct SchurTables {
-  static constexpr int kC = 32;  // chunk rows of the interior solve (schur.hip kChunk)
+  static constexpr int kC = CFDJ_SCHUR_CHUNK;  // chunk rows of the interior solve (schur.hip)
   int rl = 0, L = 0, P = 0, K = 0;
   double inv_dy2 = 0, dy2 = 0;
   double *cinv = nullptr, *corr = nullptr, *g = nullptr;

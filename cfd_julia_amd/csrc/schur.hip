@@ -133,7 +133,7 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
 // Reads and writes each element once, whole 128-B tile rows per 8 lanes.  All pivots and
 // coefficients are built on the host in long double from e_m = d_m + 2/dy^2 (exact), so
 // the near-singular low modes lose nothing to cancellation (host_common.hpp).
-constexpr int kChunk = 32;
+constexpr int kChunk = CFDJ_SCHUR_CHUNK;
 
 // K chunks per mode, MW modes per workgroup (8 = a whole tile; 4 = half a tile for the
 // 128-chunk slabs, so MW K stays within the 1024-thread / register budget).
@@ -298,7 +298,7 @@ void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
 #ifndef CFDJ_SCHUR_MW128
 #define CFDJ_SCHUR_MW128 4
 #endif
-    constexpr int MW = K >= 128 ? CFDJ_SCHUR_MW128 : (K >= 64 ? CFDJ_SCHUR_MW64 : 8);
+    constexpr int MW = K >= 256 ? 4 : K >= 128 ? CFDJ_SCHUR_MW128 : (K >= 64 ? CFDJ_SCHUR_MW64 : 8);
     hipLaunchKernelGGL((schur_solve_kernel<K, MW>), dim3(a.L / MW), dim3(MW * K), 0, st, a);
   }
 }
