@@ -293,10 +293,15 @@ __device__ __forceinline__ void load_inv(InvLoads<L>& ld, const double2* __restr
   // uniform row offset in the base pointer, 32-bit per-lane offsets (sidx(m, y0 + qq) =
   // sidx(m, qq) + sidx(0, y0) in both layouts)
   const double2* base = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
+  // the lane offsets are recomputed at every call from an opaque copy of the thread index:
+  // hoisted out of the item loop they were 16 64-bit addresses, spilled to scratch and
+  // reloaded between the prefetch loads (each reload waiting behind the earlier loads)
+  int tx = threadIdx.x;
+  asm volatile("" : "+v"(tx));
 #pragma unroll
   for (int i = 0; i < C::PAIRS; ++i) {
     int qq, m;
-    pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+    pair_index<L>(tx + i * C::THREADS, qq, m);
     ld.xm[i] = base[(unsigned)sidx<TILE>(m, qq, M)];
     ld.xp[i] = base[(unsigned)sidx<TILE>((L - m) & (L - 1), qq, M)];  // m = 0: unused
     if (m == 0) ld.xh = base[(unsigned)sidx<TILE>(L / 2, qq, M)];
