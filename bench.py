@@ -127,6 +127,11 @@ def main():
     n_gpus = max(world, 1)
     if args.gpus != n_gpus and world > 1:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    # RCCL prints its version banner on stdout at communicator init: send everything the
+    # libraries write to fd 1 to stderr, so stdout carries only the one JSON line
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
 
     import numpy as np
     import torch
@@ -310,7 +315,8 @@ def main():
                       or os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(nx, ny, args.cpu_steps, workers)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(line) + "\n").encode())
     h.close()
     if world > 1:
         dist.destroy_process_group()
