@@ -15,7 +15,10 @@ namespace cfdj {
 
 namespace {
 
-constexpr int kWavesPerBlock = 4;
+#ifndef CFDJ_STAGE_WPB
+#define CFDJ_STAGE_WPB 4  // wavefronts per stage-kernel workgroup
+#endif
+constexpr int kWavesPerBlock = CFDJ_STAGE_WPB;
 constexpr int kColsPerWave = 2 * kWave;  // two x-adjacent points per lane (16-B loads)
 
 __device__ __forceinline__ const double* row_ptr(const double* a, const double* lo,
@@ -28,7 +31,7 @@ __device__ __forceinline__ const double* row_ptr(const double* a, const double* 
 // come from lane shuffles, the two wave-edge values from one masked load each.  Four
 // independent wavefronts per 256-thread workgroup take four consecutive row chunks.
 template <int STAGE>
-__global__ __launch_bounds__(256) void vm_stage_kernel(const StageParams p) {
+__global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const StageParams p) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
   const int nx = p.nx, ny = p.ny;
