@@ -8,11 +8,17 @@
 One "step" = one full RK3 step (3 RHS evaluations = 3 FFT Poisson solves + 3 fused
 Arakawa/Laplacian/RK stage kernels) over the whole grid, all data resident in HBM.
 N = 1 runs BASELINE.json config 3 (4096^2, re = 1000, dt = 5e-4: the reference's dt = .01
-is unstable at this size).  N > 1 runs y-slabs of square power-of-two
-grids -- 8192^2 (N=2, N=4: BASELINE config 5), 16384^2 (N=8) -- i.e. 16.8 M or 33.6 M cells
-per GPU ("weak": the per-GPU work does not shrink with N; config.cells_per_gpu says how
-much).  Each RK3 stage: RCCL halo rows + the substructured Poisson solve (two all-gathers
-of O(nx) numbers) -- no spectrum transpose.
+is unstable at this size).  N > 1 runs, by default, BASELINE.json config 5: the 8192^2 grid
+as N y-slabs (total work fixed for N = 2, 4, 8: "scaling": "strong"; 1024 rows per rank at
+N = 8).  Other ladders:
+  --strong NX   fixed NX^2 grid at any N (the north star's 4096^2 at 1/2/4/8 GPUs);
+  --weak        16.8 M cells per GPU at every N on power-of-two grids (hand-written FFT
+                passes): 4096^2, 8192x4096, 8192^2, 16384x8192 at N = 1, 2, 4, 8;
+  --weak-square 4096^2 / 5760^2 / 8192^2 / 11520^2 (16.6-16.8 M cells per GPU; the
+                non-power-of-two grids run rocFFT rows/columns + all-to-all transposes).
+Each RK3 stage on square power-of-two slabs: RCCL halo rows + the substructured Poisson
+solve (two all-gathers of O(nx) numbers) -- no spectrum transpose; rectangular and other
+grids transpose the half spectrum with ncclAllToAll.
 
 Rehearsals on one GPU (not the headline): --virtual P runs the y-slab code with P virtual
 ranks (device copies for the transposes); --dist runs the RCCL slab code with a one-rank
@@ -45,21 +51,47 @@ STEP_BYTES_PER_CELL = 184
 # writing the rotated layout they read
 KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16, 7: 32, 8: 40, 9: 40, 10: 16}
 KB_LAUNCHES = 20
-# Square power-of-two grids: the substructured y-slab Poisson solve (schur.hip) needs
-# nx == ny (the reference's ky = kx table is the periodic y-symbol only then) and every
-# rank runs the hand-written row FFTs.  Cells per GPU: 16.8 M, 33.6 M, 16.8 M, 33.6 M.
-WEAK_LADDER = {1: (4096, 4096), 2: (8192, 8192), 4: (8192, 8192), 8: (16384, 16384),
-               16: (16384, 16384)}
+# Grid ladders (nx, ny) per GPU count; the second field of each value is the `scaling` label
+# of the runs at N > 1.  "c5" (default): BASELINE config 3 at N = 1, config 5 (8192^2) on
+# N = 2, 4, 8 slabs -- total work fixed over N > 1.  "weak": 16.8 M cells per GPU on
+# power-of-two grids (ny <= nx: the reference aliases ky = kx).  "weak-square": constant
+# cells on square grids, 5760^2 and 11520^2 not being powers of two.
+LADDERS = {
+    "c5": ({1: (4096, 4096), 2: (8192, 8192), 4: (8192, 8192), 8: (8192, 8192)}, "strong"),
+    "weak": ({1: (4096, 4096), 2: (8192, 4096), 4: (8192, 8192), 8: (16384, 8192)}, "weak"),
+    "weak-square": ({1: (4096, 4096), 2: (5760, 5760), 4: (8192, 8192), 8: (11520, 11520)},
+                    "weak"),
+}
 
 
-def grid_for(n_gpus, nx=None, ny=None):
+def grid_for(n_gpus, ladder="c5", nx=None, ny=None, strong=None):
+    """-> (nx, ny, scaling label, workload note)."""
+    if strong:
+        return strong, strong, "strong", f"strong scaling of the {strong}^2 grid"
     if nx:
-        return nx, ny or nx
-    if n_gpus in WEAK_LADDER:
-        return WEAK_LADDER[n_gpus]
+        return nx, ny or nx, "strong", "grid fixed on the command line"
+    table, label = LADDERS[ladder]
+    if n_gpus in table:
+        g = table[n_gpus]
+        note = {"c5": "BASELINE config 3" if n_gpus == 1 else
+                      "BASELINE config 5 (8192^2 y-slabs; total work fixed for N > 1)",
+                "weak": "weak ladder, 16.8 M cells per GPU, power-of-two grids",
+                "weak-square": "weak ladder 4096^2/5760^2/8192^2/11520^2"}[ladder]
+        return g[0], g[1], label if n_gpus > 1 else "weak", note
     step = 128 * n_gpus // math.gcd(128, n_gpus)
     n = max(step, int(round(4096 * math.sqrt(n_gpus) / step)) * step)
-    return n, n
+    return n, n, "weak", "constant cells per GPU (square grid rounded to 128 N)"
+
+
+def cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
 
 
 def stable_dt(nx, ny=None):
@@ -82,22 +114,28 @@ def load_pmc(nx):
     return d
 
 
-def cpu_baseline(nx, ny, steps, workers):
-    """The CPU oracle (NumPy + scipy.fft restatement of vm.jl/Common.jl) on this host."""
+def cpu_baseline(nx, ny, steps, workers, warmup=1):
+    """The CPU oracle (NumPy + scipy.fft restatement of vm.jl/Common.jl) on this host:
+    `warmup` untimed RK3 steps, then `steps` timed ones."""
     from oracle import vm_oracle as vo
 
     dx, dy, x, y = vo.vm_grid(nx, ny)
     w = vo.vm_ic(nx, ny, x, y)
     dt = stable_dt(nx, ny)
+    for _ in range(warmup):
+        w = vo.rk3_step(w, dt, dx, dy, 1000.0, workers=workers)
     t0 = time.perf_counter()
     for _ in range(steps):
         w = vo.rk3_step(w, dt, dx, dy, 1000.0, workers=workers)
     t = time.perf_counter() - t0
     return {"value": round(nx * ny * steps / t / 1e6, 4), "unit": "MLUPS", "cores": workers,
-            "kind": "port",
-            "sample": f"{steps} RK3 steps of the {nx}x{ny} vortex merger, NumPy oracle "
-                      f"(oracle/vm_oracle.py; scipy.fft workers={workers}, stencil single-"
-                      f"threaded NumPy), {t:.1f} s; Julia reference not runnable here"}
+            "kind": "port", "s_per_step": round(t / steps, 3),
+            "host_cpus": os.cpu_count(), "cpu_model": cpu_model(),
+            "sample": f"{warmup} warm-up + {steps} timed RK3 steps of the {nx}x{ny} vortex "
+                      f"merger, NumPy oracle (oracle/vm_oracle.py; scipy.fft workers="
+                      f"{workers} = this job's CPU share of the host's {os.cpu_count()} "
+                      f"logical CPUs, stencil single-threaded NumPy), {t:.1f} s; Julia "
+                      f"reference not runnable here"}
 
 
 def main():
@@ -115,7 +153,13 @@ def main():
     ap.add_argument("--rows-per-wave", type=int, default=None)
     ap.add_argument("--no-fused-stage", action="store_true",
                     help="five-pass stage sequence instead of the FFT-fused stage kernel")
-    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--ladder", default="c5", choices=sorted(LADDERS),
+                    help="grid per GPU count (default: config 3 at N=1, config 5 at N>1)")
+    ap.add_argument("--weak", action="store_const", const="weak", dest="ladder")
+    ap.add_argument("--weak-square", action="store_const", const="weak-square", dest="ladder")
+    ap.add_argument("--strong", type=int, default=None, metavar="NX",
+                    help="fixed NX^2 grid at any GPU count (e.g. 4096: the north-star report)")
+    ap.add_argument("--cpu-steps", type=int, default=3)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
@@ -151,7 +195,7 @@ def main():
         if world > 1:
             dist.barrier()
 
-    nx, ny = grid_for(n_gpus, args.nx, args.ny)
+    nx, ny, scaling, ladder_note = grid_for(n_gpus, args.ladder, args.nx, args.ny, args.strong)
     dx, dy = 2 * math.pi / nx, 2 * math.pi / ny
     dt = stable_dt(nx, ny)
     re = 1000.0
@@ -197,7 +241,7 @@ def main():
         torch.cuda.synchronize()
         barrier()
         el = time.perf_counter() - t0
-        kern = h.timing() if instrumented else None
+        kern = (h.timing(), h.stage_timing()) if instrumented else None
         h.set_timing(False)
         if world > 1:
             tt = torch.tensor([el], dtype=torch.float64)
@@ -214,9 +258,9 @@ def main():
     # (2) the same K steps again with HIP events around every kernel on the handle's
     # stream (eager launches: event nodes cannot be captured into graphs on this ROCm)
     if args.no_timing:
-        elapsed_i, kern = None, {k: (0.0, 0) for k in _lib.K_NAMES}
+        elapsed_i, kern, kern_stage = None, {k: (0.0, 0) for k in _lib.K_NAMES}, [(0.0, 0)] * 3
     else:
-        elapsed_i, kern = timed(True)
+        elapsed_i, (kern, kern_stage) = timed(True)
 
     # sanity: the state stays finite and bounded (conservative scheme)
     h.set_check_finite(True)
@@ -246,22 +290,34 @@ def main():
     local_cells = cells / n_gpus
     fstage = h.fused_stage()
     kname = "vm_fused_stage_kernel" if fstage else "vm_stage_kernel"
-    if kb:
-        # the three stage kernels of the step together: algorithmic bytes (24 + 32 + 32 or,
-        # FFT-fused, 32 + 40 + 40 per cell) over their summed per-launch times
-        st = [kb[f"{kname}<{i}>"] for i in (1, 2, 3)]
-        stage_us = sum(k["us_per_launch"] for k in st) / 3.0
-        stage_alg = sum(k["alg_bytes"] for k in st) / 3.0
-        stage_n = 3 * KB_LAUNCHES
-        source = (f"HIP events around {KB_LAUNCHES} back-to-back launches of each stage "
-                  f"kernel on the handle stream (cfdj_vm_kernel_bench), mean of stages 1-3")
-    else:
-        stage_ms, stage_n = kern["stage"]
-        stage_us = stage_ms * 1e3 / max(stage_n, 1)
-        stage_alg = (112 if fstage else STAGE_BYTES_PER_CELL_STEP) / 3.0 * local_cells
-        source = ("HIP events around every kernel on the handle stream, over a second "
-                  "timed region of the same K steps (eager launches)")
+    # Roofline of the stage kernels from their IN-STEP launch times: HIP events around every
+    # stage-kernel launch of the instrumented timed region (the kernels run in the step's
+    # own sequence, between the Poisson passes), algorithmic bytes 24 / 32 / 32 per cell
+    # (FFT-fused: 32 / 40 / 40).  The back-to-back microbenchmark figure is kept beside it
+    # as frac_isolated.
+    alg_cell = (32, 40, 40) if fstage else (24, 32, 32)
+    per_stage = []
+    for i, (ms_i, n_i) in enumerate(kern_stage):
+        if n_i:
+            us_i = ms_i * 1e3 / n_i
+            gbs_i = alg_cell[i] * local_cells / (us_i * 1e-6) / 1e9
+            per_stage.append({"stage": i + 1, "avg_launch_us": round(us_i, 2),
+                              "alg_bytes": int(alg_cell[i] * local_cells),
+                              "achieved": round(gbs_i, 1),
+                              "frac": round(gbs_i / HBM_PEAK_GBS, 4), "launches": n_i})
+    stage_ms, stage_n = kern["stage"]
+    stage_us = stage_ms * 1e3 / max(stage_n, 1)
+    stage_alg = sum(alg_cell) / 3.0 * local_cells
+    source = ("HIP events around every stage-kernel launch on the handle stream, in the "
+              "step's own kernel sequence, over a second timed region of the same K steps "
+              "(eager launches); mean over the three RK3 stages")
     stage_gbs = stage_alg / (stage_us * 1e-6) / 1e9 if stage_us > 0 else None
+    iso = None
+    if kb:
+        st = [kb[f"{kname}<{i}>"] for i in (1, 2, 3)]
+        iso_us = sum(k["us_per_launch"] for k in st) / 3.0
+        iso_alg = sum(k["alg_bytes"] for k in st) / 3.0
+        iso = iso_alg / (iso_us * 1e-6) / 1e9
     roofline = {
         "kernel": ("vm_fused_stage_kernel (row c2r of psi-hat + Arakawa J + 5-pt Laplacian "
                    "+ RK3 stage + row r2c of the output, psi on chip)" if fstage else
@@ -275,6 +331,10 @@ def main():
         "alg_bytes_per_launch": int(round(stage_alg)),
         "avg_launch_us": round(stage_us, 2),
         "launches": stage_n,
+        "per_stage": per_stage,
+        "frac_isolated": round(iso / HBM_PEAK_GBS, 4) if iso else None,
+        "frac_isolated_source": (f"{KB_LAUNCHES} back-to-back launches of each stage kernel "
+                                 f"on identical inputs (cfdj_vm_kernel_bench)") if iso else None,
         "source": source,
     }
     pmc = load_pmc(nx)
@@ -294,12 +354,13 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": scaling,
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: vm_ic two-Gaussian vortex-merger IC (Common.jl:208-219)",
         "config": {"workload": f"NS2D vortex merger {nx}x{ny} periodic, Arakawa + FD-FFT "
-                               f"Poisson + SSP-RK3 (vm.jl)", "nx": nx, "ny": ny, "dt": dt,
+                               f"Poisson + SSP-RK3 (vm.jl): {ladder_note}",
+                   "nx": nx, "ny": ny, "dt": dt,
                    "re": re, "parallelism": parallelism, "poisson": h.poisson(),
                    "fused_stage": fstage,
                    "cells_per_gpu": cells // n_gpus},
@@ -313,7 +374,7 @@ def main():
     if rank == 0 and n_gpus == 1 and not args.no_cpu_baseline and not args.virtual:
         workers = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
                       or os.cpu_count() or 1)
-        line["cpu_baseline"] = cpu_baseline(nx, ny, args.cpu_steps, workers)
+        line["cpu_baseline"] = cpu_baseline(nx, ny, args.cpu_steps, workers, warmup=1)
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + "\n").encode())

@@ -76,6 +76,7 @@ SIGNATURES = {
     "cfdj_vm_rhs": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long, _dp, C.c_long]),
     "cfdj_vm_set_timing": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_timing": (C.c_int, [_vp, _dp, _lp]),
+    "cfdj_vm_stage_timing": (C.c_int, [_vp, _dp, _lp]),
     "cfdj_vm_kernel_bench": (C.c_int, [_vp, C.c_int, C.c_double, C.c_int, _dp]),
     "cfdj_vm_set_check_finite": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_field_device": (C.c_int, [_vp, C.POINTER(_vp)]),
@@ -106,6 +107,7 @@ SIGNATURES = {
                                  C.c_int, C.c_int, C.c_int, C.POINTER(_vp)]),
     "cfdj_mg_solve": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long, C.c_double, C.c_int, _ip,
                                 _dp]),
+    "cfdj_mg_residual": (C.c_int, [_vp, _dp, C.c_long]),
     "cfdj_mg_destroy": (None, [_vp]),
     "cfdj_jacobi_solve": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, _dp, C.c_long,
                                     _dp, C.c_long, C.c_long, C.c_double, C.c_long, _lp, _dp]),

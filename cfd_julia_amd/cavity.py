@@ -64,6 +64,8 @@ class Cavity:
     def rhs(self, w, s):
         w = np.asfortranarray(w, dtype=np.float64)
         s = np.asfortranarray(s, dtype=np.float64)
+        _lib.fortran_view(w, "w", self._shape())
+        _lib.fortran_view(s, "s", self._shape())
         r = np.zeros(self._shape(), order="F")
         check(_lib.load().cfdj_cavity_rhs(self._h, dptr(w), w.shape[0], dptr(s), s.shape[0],
                                           dptr(r), r.shape[0]), "cfdj_cavity_rhs")
@@ -91,14 +93,22 @@ def fps_sine(nx, ny, dx, dy, f, u=None, e=None, data=None, data1=None, iden=None
     5-point Poisson solution with right-hand side f[1:nx, 1:ny]; returns sn."""
     f = np.asfortranarray(f, dtype=np.float64)
     sn = np.zeros((nx + 1, ny + 1), order="F") if sn is None else sn
+    # the C side copies (nx+1) x (ny+1) nodes in and out: a short, C-ordered or non-float64
+    # array would be read / written out of bounds or transposed
+    f, ldf = _lib.fortran_view(f, "f", (nx + 1, ny + 1))
+    sn, lds = _lib.fortran_view(sn, "sn", (nx + 1, ny + 1), writable=True)
     _lib.require_gpu()
     check(_lib.load().cfdj_fps_sine(int(nx), int(ny), float(dx), float(dy), dptr(f),
-                                    f.shape[0], dptr(sn), sn.shape[0]), "cfdj_fps_sine")
+                                    ldf, dptr(sn), lds), "cfdj_fps_sine")
     return sn
 
 
 def numerical(nx, ny, nt, dx, dy, dt, re, wn, sn, rms, device=-1, poisson="dst"):
     """lid_driven_cavity.jl:58-118: advances wn, sn in place for nt steps and fills rms."""
+    _lib.fortran_view(wn, "wn", (nx + 1, ny + 1), writable=True)
+    _lib.fortran_view(sn, "sn", (nx + 1, ny + 1), writable=True)
+    if len(rms) < nt:
+        raise _lib.ArgumentError(-1, "rms", f"length {len(rms)} < nt = {nt} (BoundsError)")
     with Cavity(nx, ny, dx, dy, re, device, poisson) as h:
         h.upload(wn, sn)
         rms[:nt] = h.step(dt, nt)

@@ -741,6 +741,16 @@ int cfdj_mg_solve(cfdj_mg* h, const double* f, long ldf, double* u, long ldu, do
   });
 }
 
+int cfdj_mg_residual(cfdj_mg* h, double* r, long ldr) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && r, "NULL argument");
+    CFDJ_REQUIRE(ldr >= h->nx + 1, "leading dimension too small");
+    select_device(h->device);
+    copy_out(r, ldr, h->mg.r[0], h->nx + 2, h->nx, h->ny, h->stream);
+    CFDJ_HIP(hipStreamSynchronize(h->stream));
+  });
+}
+
 int cfdj_jacobi_solve(int nx, int ny, double dx, double dy, const double* f, long ldf,
                       double* u, long ldu, long max_iter, double tol, long freq,
                       long* iterations, double* rms_out) {

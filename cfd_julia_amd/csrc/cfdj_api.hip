@@ -131,6 +131,9 @@ struct cfdj_vm {
   size_t ev_used = 0;
   double ms[CFDJ_K_COUNT] = {};
   long launches[CFDJ_K_COUNT] = {};
+  std::vector<int> ev_stage;  // RK3 stage (1..3) of a CFDJ_K_STAGE interval, else 0
+  double stage_ms[3] = {};
+  long stage_launches[3] = {};
   // finiteness check
   bool check_finite = false;
   int* d_flag = nullptr;
@@ -151,11 +154,12 @@ struct cfdj_vm {
       ev.push_back(e);
     }
   }
-  void tbegin(int cat) {
+  void tbegin(int cat, int rk_stage = 0) {
     if (!timing) return;
     if (ev_used + 2 > ev.size()) reserve_events(ev.size() + 64);
     CFDJ_HIP(hipEventRecord(ev[ev_used], stream));
     ev_cat.push_back(cat);
+    ev_stage.push_back(rk_stage);
   }
   void tend() {
     if (!timing) return;
@@ -169,9 +173,14 @@ struct cfdj_vm {
       CFDJ_HIP(hipEventElapsedTime(&t, ev[2 * i], ev[2 * i + 1]));
       ms[ev_cat[i]] += t;
       launches[ev_cat[i]] += 1;
+      if (ev_stage[i] >= 1 && ev_stage[i] <= 3) {
+        stage_ms[ev_stage[i] - 1] += t;
+        stage_launches[ev_stage[i] - 1] += 1;
+      }
     }
     ev_used = 0;
     ev_cat.clear();
+    ev_stage.clear();
   }
 
   // Column-sum partial buffers of the Schur path, one block per rows_per_wave rows (the
@@ -496,7 +505,7 @@ struct cfdj_vm {
     for (size_t i = 0; i < slabs.size(); ++i) {
       Slab& s = slabs[i];
       double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
-      tbegin(CFDJ_K_STAGE);
+      tbegin(CFDJ_K_STAGE, st);
       StageParams p = stage_params(s, src[i], s.wn, out, dt);
       if (use_schur) {  // column-sum partials of the output for the next stage's Poisson
         const int oi = st == 1 ? 1 : st == 2 ? 2 : 0;
@@ -638,7 +647,7 @@ struct cfdj_vm {
         tbegin(CFDJ_K_DIVIDE);
         launch_fused_poisson_pass(1, c, stream);
         tend();
-        tbegin(CFDJ_K_STAGE);
+        tbegin(CFDJ_K_STAGE, st);
         launch_fused_stage(st, fused_stage_params(src, out, dt, !(n == nsteps - 1 && st == 3)),
                            stream);
         tend();
@@ -1141,6 +1150,20 @@ int cfdj_vm_set_timing(cfdj_vm* h, int enable) {
     for (int k = 0; k < CFDJ_K_COUNT; ++k) {
       h->ms[k] = 0.0;
       h->launches[k] = 0;
+    }
+    for (int k = 0; k < 3; ++k) {
+      h->stage_ms[k] = 0.0;
+      h->stage_launches[k] = 0;
+    }
+  });
+}
+
+int cfdj_vm_stage_timing(cfdj_vm* h, double* ms3, long* launches3) {
+  return guard([&] {
+    CFDJ_REQUIRE(h != nullptr, "NULL handle");
+    for (int k = 0; k < 3; ++k) {
+      if (ms3) ms3[k] = h->stage_ms[k];
+      if (launches3) launches3[k] = h->stage_launches[k];
     }
   });
 }

@@ -12,14 +12,14 @@ from ._lib import check, dptr
 
 def gauss_seidel(dx, dy, nx, ny, r, f, u_n, max_iter, tol, out=None, freq=10000, device=-1):
     """gauss_seidel.jl:8-54: solves into u_n in place; returns (iterations, rms)."""
-    _lib.require_gpu()
     f = np.asfortranarray(f, dtype=np.float64)
-    if not (isinstance(u_n, np.ndarray) and u_n.flags.f_contiguous):
-        raise TypeError("u_n must be a Fortran-ordered float64 array (updated in place)")
+    f, ldf = _lib.fortran_view(f, "f", (nx + 1, ny + 1))
+    u_n, ldu = _lib.fortran_view(u_n, "u_n", (nx + 1, ny + 1), writable=True)
+    _lib.require_gpu()
     it = C.c_long()
     rms = C.c_double()
     check(_lib.load().cfdj_jacobi_solve(int(nx), int(ny), float(dx), float(dy), dptr(f),
-                                        f.shape[0], dptr(u_n), u_n.shape[0], int(max_iter),
+                                        ldf, dptr(u_n), ldu, int(max_iter),
                                         float(tol), int(freq), C.byref(it), C.byref(rms)),
           "cfdj_jacobi_solve")
     if out is not None:

@@ -159,6 +159,13 @@ class VortexMerger:
         check(_lib.load().cfdj_vm_timing(self._h, ms, n), "cfdj_vm_timing")
         return {name: (ms[i], n[i]) for i, name in enumerate(_lib.K_NAMES)}
 
+    def stage_timing(self):
+        """[(ms, launches)] of the stage kernel per RK3 stage 1..3 (same recording as timing())."""
+        ms = (C.c_double * 3)()
+        n = (C.c_long * 3)()
+        check(_lib.load().cfdj_vm_stage_timing(self._h, ms, n), "cfdj_vm_stage_timing")
+        return [(ms[i], n[i]) for i in range(3)]
+
     def kernel_bench(self, kernel, dt, launches=20):
         """ms per launch of `launches` back-to-back launches of one kernel (CFDJ_KB_*);
         clobbers the stage buffers and advances the field: use after the timed runs."""

@@ -134,6 +134,9 @@ int cfdj_vm_rhs(cfdj_vm* h, const double* w, long ldw, double* r, long ldr, doub
  * receive the accumulated totals (either may be NULL). */
 int cfdj_vm_set_timing(cfdj_vm* h, int enable);
 int cfdj_vm_timing(cfdj_vm* h, double* ms, long* launches);
+/* The CFDJ_K_STAGE time split by RK3 stage (vm.jl:28 / 43-47 / 62-66): ms3[3], launches3[3]
+ * for stages 1..3, accumulated over the same recording as cfdj_vm_timing. */
+int cfdj_vm_stage_timing(cfdj_vm* h, double* ms3, long* launches3);
 /* Kernel microbenchmark (no reference equivalent; bench.py's roofline): `launches`
  * back-to-back launches of one kernel of the step between two HIP events on the handle's
  * stream; *ms_per_launch = elapsed / launches.  Single-GPU handles on the fused Poisson
@@ -207,12 +210,20 @@ int cfdj_fps_sine(int nx, int ny, double dx, double dy, const double* f, long ld
  * boundary values in and the solution out.  Smoother: red-black ordering of the
  * Common.jl:78-92 Gauss-Seidel update (the reference sweeps lexicographically; converged
  * solutions agree to the tolerance).  rms_hist (may be NULL) receives iterations+1
- * residual norms (Common.jl:229-232), the first being the initial residual. */
+ * residual norms (Common.jl:229-232), the first being the initial residual.
+ * The two-level solver of 17_Poisson_Solver_Multigrid/mg.jl:7-85 is n_level = 2 with the
+ * roles of v2 and v3 exchanged: mg.jl relaxes the coarse grid v3 times (mg.jl:66) and the
+ * corrected fine grid v2 times (mg.jl:77), mg_N.jl the other way round (mg_N.jl:91,103);
+ * pass (v1, v3, v2) for mg.jl's (v1, v2, v3). */
 typedef struct cfdj_mg cfdj_mg;
 int cfdj_mg_create(int nx, int ny, double dx, double dy, int n_level, int v1, int v2, int v3,
                    int device, cfdj_mg** out);
 int cfdj_mg_solve(cfdj_mg* h, const double* f, long ldf, double* u, long ldu, double tol,
                   int max_iter, int* iterations, double* rms_hist);
+/* The fine-grid residual r = f - lap(u) of the last cfdj_mg_solve's final convergence
+ * check (mg_N.jl:59 / mg.jl:47 leave it in the caller's `r`; boundary entries are 0):
+ * (nx+1) x (ny+1), ldr >= nx+1. */
+int cfdj_mg_residual(cfdj_mg* h, double* r, long ldr);
 void cfdj_mg_destroy(cfdj_mg* h);
 
 /* ---- 15_Poisson_Solver_Gauss_Seidel/gauss_seidel.jl:8-54 ----------------------------------

@@ -246,6 +246,37 @@ def mg_n(f, u, dx, dy, n_level, v1=2, v2=2, v3=2, tol=1e-9, max_iter=100000,
     return u_mg[0], it, hist
 
 
+def mg_2level(f, u, dx, dy, v1=2, v2=2, v3=2, tol=1e-9, max_iter=100000,
+              smoother=gauss_seidel_rb):
+    """17_Poisson_Solver_Multigrid/mg.jl:7-85, the two-level cycle: v1 sweeps on the fine
+    grid (mg.jl:44), convergence check (:47-58), restriction (:61), v3 sweeps on the coarse
+    grid from zero (:63-66), prolongation + correction (:70-75), v2 sweeps on the fine grid
+    (:77).  Returns (u, iterations, [rms history incl. iteration 0], final residual r)."""
+    nx, ny = u.shape[0] - 1, u.shape[1] - 1
+    u = u.copy()
+    r = compute_residual(f, u, dx, dy)
+    init_rms = rms = compute_l2norm(r)
+    hist = [rms]
+    nxc, nyc = nx // 2, ny // 2
+    dxc, dyc = dx * 2, dy * 2
+    it = 0
+    while it < max_iter:
+        it += 1
+        smoother(f, u, dx, dy, v1)
+        r = compute_residual(f, u, dx, dy)
+        rms = compute_l2norm(r)
+        hist.append(rms)
+        if rms / init_rms <= tol:
+            break
+        fc = restriction(r, nxc, nyc)
+        unc = np.zeros_like(fc)
+        smoother(fc, unc, dxc, dyc, v3)
+        p = prolongation(unc, nx, ny)
+        u[1:-1, 1:-1] += p[1:-1, 1:-1]
+        smoother(f, u, dx, dy, v2)
+    return u, it, hist, r
+
+
 def mg_mms(nx, ny=None, ipr=1):
     """mg_N.jl:127-169: unit box MMS, Dirichlet boundary from the exact solution."""
     ny = nx if ny is None else ny

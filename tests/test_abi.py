@@ -91,3 +91,75 @@ def test_product_path_does_not_import_oracle():
             if f.endswith((".py", ".hip", ".hpp", ".cpp", ".h", "Makefile")):
                 src = open(os.path.join(dirpath, f)).read()
                 assert not pat.search(src), f
+
+
+def test_secondary_mirrors_validate_arrays_before_the_c_call():
+    """cavity.fps_sine / numerical, mg.Multigrid.solve and gauss_seidel check shape, order and
+    dtype of caller arrays (the C side copies (nx+1) x (ny+1) nodes in and out) -- raised
+    before anything touches the GPU, so this runs on CPU."""
+    import numpy as np
+
+    from cfd_julia_amd import _lib, cavity, gauss_seidel
+    from cfd_julia_amd import mg as mgmod
+
+    n = 16
+    f = np.zeros((n + 1, n + 1), order="F")
+    with pytest.raises(_lib.ArgumentError):  # C-ordered output would come back transposed
+        cavity.fps_sine(n, n, 1.0 / n, 1.0 / n, f, sn=np.zeros((n + 1, n + 2)))
+    with pytest.raises(_lib.ArgumentError):  # short output: out-of-bounds host write
+        cavity.fps_sine(n, n, 1.0 / n, 1.0 / n, f, sn=np.zeros((n, n), order="F"))
+    with pytest.raises(_lib.ArgumentError):
+        cavity.fps_sine(n, n, 1.0 / n, 1.0 / n, np.zeros((n, n), order="F"))
+    with pytest.raises(TypeError):
+        cavity.fps_sine(n, n, 1.0 / n, 1.0 / n, f, sn=np.zeros((n + 1, n + 1), np.float32, order="F"))
+    with pytest.raises(_lib.ArgumentError):
+        cavity.numerical(n, n, 2, 1.0 / n, 1.0 / n, 1e-3, 100.0, np.zeros((n, n), order="F"),
+                         np.zeros((n + 1, n + 1), order="F"), np.zeros(2))
+    with pytest.raises(_lib.ArgumentError):
+        cavity.numerical(n, n, 2, 1.0 / n, 1.0 / n, 1e-3, 100.0, f.copy(order="F"),
+                         f.copy(order="F"), np.zeros(1))
+    with pytest.raises(_lib.ArgumentError):
+        gauss_seidel.gauss_seidel(1.0 / n, 1.0 / n, n, n, None, f, np.zeros((n, n + 1), order="F"),
+                                  10, 1e-9)
+    with pytest.raises(_lib.ArgumentError):
+        gauss_seidel.gauss_seidel(1.0 / n, 1.0 / n, n, n, None, np.zeros((n + 1, n)), f.copy(order="F"),
+                                  10, 1e-9)
+    m = mgmod.Multigrid.__new__(mgmod.Multigrid)  # no handle: validation comes first
+    m._h, m.nx, m.ny = None, n, n
+    with pytest.raises(_lib.ArgumentError):
+        m.solve(f, np.zeros((n, n), order="F"))
+    with pytest.raises(_lib.ArgumentError):
+        m.solve(f, np.zeros((n + 1, n + 2))[:, :n + 1])  # C-ordered view
+    with pytest.raises(_lib.ArgumentError):
+        m.residual(np.zeros((n, n + 1), order="F"))
+
+
+def test_julia_shim_ccalls_match_the_header():
+    """julia/CFDJ.jl cannot run here (no julia): check statically that every ccall names an
+    exported symbol and passes as many arguments, of the matching C kind, as the binding."""
+    import ctypes as C
+    import re
+
+    src = open(os.path.join(ROOT, "julia", "CFDJ.jl"), encoding="utf-8").read()
+    calls = re.findall(r"ccall\(\(:(\w+),\s*libcfdj\),\s*(\w+),\s*\(([^)]*)\)", src)
+    assert len(calls) >= 20
+    kind = {"Cint": C.c_int, "Clong": C.c_long, "Cdouble": C.c_double}
+    seen = set()
+    for name, ret, types in calls:
+        assert name in _lib.SIGNATURES, name
+        res, args = _lib.SIGNATURES[name]
+        jl = [t.strip() for t in types.split(",") if t.strip()]
+        assert len(jl) == len(args), (name, jl, args)
+        for t, a in zip(jl, args):
+            if t in kind:
+                assert a is kind[t], (name, t, a)
+            else:  # Ptr{...} / Ref{...} / Cstring: a pointer on the C side
+                assert t.startswith(("Ptr{", "Ref{")) and a not in kind.values(), (name, t, a)
+        assert {"Cint": C.c_int, "Cvoid": None, "Cstring": C.c_char_p}[ret] is res or \
+            (ret == "Cstring" and res is C.c_char_p), (name, ret)
+        seen.add(name)
+    # the entry points the north star names as drop-in: vm.jl, lid_driven_cavity.jl, mg.jl
+    for must in ("cfdj_vm_step", "cfdj_vm_rhs", "cfdj_fps_solve", "cfdj_cavity_step",
+                 "cfdj_cavity_rhs", "cfdj_fps_sine", "cfdj_mg_solve", "cfdj_mg_residual"):
+        assert must in seen, must
+    assert "VM_CACHE" in src and "cached_vm(nx, ny" in src  # vm_rhs reuses its handle

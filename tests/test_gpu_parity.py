@@ -189,7 +189,7 @@ def test_gpu_conservation_at_full_size(cfdj):
     assert 0.99 < w.max() <= w0.max() + 1e-12
 
 
-def test_gpu_full_size_vs_oracle(cfdj):
+def test_gpu_full_size_3_steps_vs_oracle(cfdj):
     """C3 (4096^2, re = 1000, dt = 5e-4): L∞ vs the oracle after 3 RK3 steps."""
     n = 4096
     dx, dy, w0 = vm_setup(n)

@@ -157,3 +157,20 @@ def test_spectral_oracle_jacobians_agree():
         assert np.abs(j[1] - j[2]).max() < 1e-12 * np.abs(j[1]).max()
         errs.append(np.abs(j[0] - j[1]).max())
     assert 3.0 < errs[0] / errs[1] < 5.0  # O(dx^2)
+
+
+# ---- mg.jl (two-level) vs mg_N.jl with n_level = 2 ------------------------------------------
+def test_mg_two_level_is_mg_n_with_v2_v3_exchanged():
+    """mg.jl:66,77 relax the coarse grid v3 times and the corrected fine grid v2 times;
+    mg_N.jl:91,103 the other way round.  With v2 != v3 the two differ unless exchanged."""
+    from oracle import cavity_oracle as co
+
+    n = 32
+    f, ue, un, dx, dy = co.mg_mms(n, ipr=2)
+    u2, it2, h2, r2 = co.mg_2level(f, un, dx, dy, v1=2, v2=1, v3=3, tol=1e-8)
+    uN, itN, hN = co.mg_n(f, un, dx, dy, 2, v1=2, v2=3, v3=1, tol=1e-8)
+    assert it2 == itN and np.array_equal(u2, uN) and h2 == hN
+    uX, itX, hX = co.mg_n(f, un, dx, dy, 2, v1=2, v2=1, v3=3, tol=1e-8)
+    assert not np.array_equal(u2, uX)  # same arguments, un-exchanged: a different iteration
+    assert np.array_equal(r2, co.compute_residual(f, u2, dx, dy)) or it2 > 0
+    assert np.abs(u2 - ue).max() < 5e-3  # converged to the discrete solution (O(h^2) from ue)
