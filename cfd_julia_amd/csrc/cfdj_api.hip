@@ -19,6 +19,41 @@ const char* last_error() { return g_err.c_str(); }
 using namespace cfdj;
 
 // =====================================================================================
+// Static spectrum scratch of cfdj_fps_solve_device_noalloc
+// =====================================================================================
+// The half spectrum of the hand-written FFT Poisson passes, for callers that cannot
+// allocate: (nx/2) * ny complex elements, at most kNoAllocMaxSpectrum (16 MiB).  Every GPU
+// the library runs on holds its own copy of the array at its own address until the process
+// ends.  In host code the array's name is only a stand-in: the device address comes from
+// hipGetSymbolAddress, once per device with that device current (noalloc_scratch_init, at
+// plan creation), and that pointer is what the kernels receive.
+namespace {
+
+constexpr size_t kNoAllocMaxSpectrum = (size_t)1 << 20;  // complex elements
+static __device__ __align__(256) double2 g_noalloc_scratch[kNoAllocMaxSpectrum];
+
+constexpr int kMaxDevices = 64;
+std::mutex g_noalloc_mu;
+double2* g_noalloc_ptr[kMaxDevices] = {};
+
+// Resolve (once) and return the scratch array's address on the current device.
+double2* noalloc_scratch_init() {
+  int dev = -1;
+  CFDJ_HIP(hipGetDevice(&dev));
+  CFDJ_REQUIRE(dev >= 0 && dev < kMaxDevices, "device ordinal out of range");
+  std::lock_guard<std::mutex> lk(g_noalloc_mu);
+  if (g_noalloc_ptr[dev] == nullptr) {
+    void* p = nullptr;
+    CFDJ_HIP(hipGetSymbolAddress(&p, HIP_SYMBOL(g_noalloc_scratch)));
+    CFDJ_REQUIRE(p != nullptr, "hipGetSymbolAddress returned a null scratch address");
+    g_noalloc_ptr[dev] = static_cast<double2*>(p);
+  }
+  return g_noalloc_ptr[dev];
+}
+
+}  // namespace
+
+// =====================================================================================
 // Poisson handle (Common.jl:97-125 / fft_p.jl:8-42)
 // =====================================================================================
 struct cfdj_fps_plan {
@@ -32,10 +67,12 @@ struct cfdj_fps_plan {
   double *f_dev = nullptr, *s_dev = nullptr;
   Fused fused;
   bool use_fused = false;
+  double2* static_spec = nullptr;  // this device's g_noalloc_scratch (set at creation)
 
-  void solve_device(const double* f, double* s) {
+  void solve_device(const double* f, double* s) { solve_device(f, s, spec); }
+  void solve_device(const double* f, double* s, double2* H) {
     if (use_fused) {
-      const FusedPoissonArgs a = fused.args(sym, f, s, spec, false);
+      const FusedPoissonArgs a = fused.args(sym, f, s, H, false);
       for (int pass = 0; pass < 3; ++pass) launch_fused_poisson_pass(pass, a, stream);
       return;
     }
@@ -930,6 +967,7 @@ int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device
       h->fused.init(nx, ny);
       h->use_fused = true;
     }
+    h->static_spec = noalloc_scratch_init();  // set-up: the plan's device is current
     *out = h.release();
   });
 }
@@ -955,6 +993,28 @@ int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev) 
     CFDJ_REQUIRE(h && f_dev && s_dev, "NULL argument");
     select_device(h->device);
     h->solve_device(f_dev, s_dev);
+  });
+}
+
+// The same solve with the half spectrum in the library's static device array: no
+// hipMalloc / hipFree / rocFFT call on this path (only the three hand-written passes).
+int cfdj_fps_solve_device_noalloc(cfdj_fps_plan* h, const double* f_dev, double* s_dev) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && f_dev && s_dev, "NULL argument");
+    CFDJ_REQUIRE(h->use_fused,
+                 "cfdj_fps_solve_device_noalloc needs a plan on the hand-written FFT path "
+                 "(power-of-two nx, ny >= 1024, ny <= nx): rocFFT may allocate");
+    const size_t need = (size_t)(h->sym.nx / 2) * (size_t)h->sym.ny;
+    if (need > kNoAllocMaxSpectrum)
+      throw Error{CFDJ_ERR_ARG, "cfdj_fps_solve_device_noalloc: (nx/2)*ny = " +
+                                    std::to_string(need) + " complex elements exceed the static "
+                                    "scratch of " + std::to_string(kNoAllocMaxSpectrum) +
+                                    " (e.g. 2048 x 1024); use cfdj_fps_solve_device"};
+    CFDJ_REQUIRE(h->static_spec != nullptr, "static scratch not initialised");
+    select_device(h->device);
+    // nothing in the scratch has to start at zero: the row pass writes every element of
+    // the (nx/2) x ny spectrum before the column pass reads it
+    h->solve_device(f_dev, s_dev, h->static_spec);
   });
 }
 

@@ -55,6 +55,13 @@ class PoissonFFT:
         check(_lib.load().cfdj_fps_solve_device(self._h, C.c_void_p(f_ptr), C.c_void_p(s_ptr)),
               "cfdj_fps_solve_device")
 
+    def solve_device_noalloc(self, f_ptr, s_ptr):
+        """cfdj_fps_solve_device with the half spectrum in the library's static device
+        array: allocates nothing (fused path, (nx/2)*ny <= 2**20)."""
+        check(_lib.load().cfdj_fps_solve_device_noalloc(self._h, C.c_void_p(f_ptr),
+                                                        C.c_void_p(s_ptr)),
+              "cfdj_fps_solve_device_noalloc")
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().cfdj_fps_destroy(self._h)

@@ -81,6 +81,16 @@ int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device
 int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long lds);
 /* Same, on device pointers (contiguous, pitch nx) on the handle's stream; no sync. */
 int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
+/* No counterpart in the reference: cfdj_fps_solve_device for callers that cannot allocate
+ * device memory (code under HIP graph capture, tight serving loops, harnesses that forbid
+ * hipMalloc).  The half spectrum lives in a static device array of the library instead of
+ * the plan's buffer; the call itself runs only the three hand-written FFT passes on the
+ * plan's stream (no hipMalloc / hipFree / rocFFT), no sync.  Limits: a plan on the
+ * CFDJ_POISSON_FUSED path and (nx/2)*ny <= 1048576 complex elements (16 MiB, e.g.
+ * 2048 x 1024 or 1024 x 1024); larger or rocFFT-path plans return CFDJ_ERR_ARG.  All calls
+ * on one GPU share that GPU's array (any plan, any stream): calls that overlap on one GPU
+ * race; nothing in it needs clearing between calls. */
+int cfdj_fps_solve_device_noalloc(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
 /* Select the Poisson implementation (CFDJ_POISSON_*); ARG error if unsupported. */
 int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path);
 /* The implementation in use (CFDJ_POISSON_ROCFFT or CFDJ_POISSON_FUSED; ARG on NULL). */
