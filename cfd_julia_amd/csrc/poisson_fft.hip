@@ -83,6 +83,63 @@ __device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __res
     for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[(unsigned)in_pos<L, 0>(tid, b, r)];
 }
 
+// One work item (XR rows) of the forward row pass: stage 0 on the prefetched rows in `nxt`,
+// LDS write, refill `nxt` with the next item's rows (next_y0 >= 0), remaining stages,
+// post-processing, stores.  The 16 stores per thread are unconditional and fully unrolled,
+// and the kernel peels its first item, so every entry into the item loop carries the same
+// queue of vector-memory operations (the 16 prefetch loads, then the 16 stores): the wait
+// for the prefetched rows at the top of an item is then a counted `vmcnt` that leaves the
+// previous item's stores in flight -- their drain overlaps stage 0 instead of stalling it
+// (vmcnt completes in order; a conservative vmcnt(0) there cost a quarter of the pass).
+template <int L, bool TILE>
+__device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, double2* buf,
+                                              const double* __restrict__ f,
+                                              double2* __restrict__ H, int M, int y0,
+                                              int next_y0, int q, int tid,
+                                              const TwLds<L>& twL, const TwLds<2 * L>& twN) {
+  using P = Plan<L>;
+  using C = RowCfg<L>;
+  stage_regs<L, 0, -1>(nxt, tid, twL);
+  lds_write<L, 0>(buf, nxt, tid);
+  if (next_y0 >= 0) load_row_z<L>(nxt, f, next_y0 + q, tid);
+  __syncthreads();
+  double2 v[16];
+  run_stages<L, 1, -1, true>(buf, v, tid, twL);
+
+  // post-process, two outputs per pair: X[m] = E[m] + W^m O[m], X[L-m] likewise;
+  // slot 0 = X[0] + i X[L]; m = L/2 is its own partner (stored by the m = 0 lane, which
+  // can only occur in pair 0: later pairs start at m >= 16).  Stores go through a
+  // wave-uniform base (row y0) and 32-bit element offsets: one offset VGPR per store.
+  double2* hb = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
+#pragma unroll
+  for (int i = 0; i < C::PAIRS; ++i) {
+    int qq, m;
+    pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+    const bool z0 = i == 0 && m == 0;
+    const int mp = z0 ? L / 2 : L - m;
+    const double2* bq = lds + qq * P::ROWSTRIDE;
+    const double2 Zm = bq[padx(m)];
+    const double2 Zp = bq[padx(mp)];
+    const double2 Zc = cconj(Zp);
+    const double2 E = make_double2(0.5 * (Zm.x + Zc.x), 0.5 * (Zm.y + Zc.y));
+    const double2 D = csub(Zm, Zc);                       // = 2i O[m]
+    const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
+    const double2 WO = cmul(twN.w(m), O);
+    double2 o1 = cadd(E, WO);
+    // X[L-m] = conj(E[m]) + W^{L-m} conj(O[m]) = conj(E[m] - W^m O[m])
+    double2 o2 = cconj(csub(E, WO));
+    if (i == 0) {
+      if (z0) {  // X[L/2] = E + W^{L/2} O, W^{L/2} = -i: conj(Z[L/2])
+        o1 = make_double2(Zm.x + Zm.y, Zm.x - Zm.y);
+        o2 = Zc;
+      }
+    }
+    hb[(unsigned)sidx<TILE>(m, qq, M)] = o1;
+    hb[(unsigned)sidx<TILE>(mp, qq, M)] = o2;
+  }
+  __syncthreads();  // LDS is rewritten by the next item
+}
+
 template <int L, bool TILE>
 __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
@@ -103,45 +160,16 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
   // table fill's wait does not serialise them.
   twL.fill(twL_);
   twN.fill(twN_);
+  if (rg.count <= 0) return;
   double2 nxt[16];
-  if (rg.count > 0) load_row_z<L>(nxt, f, rg.first * C::XR + q, tid);
+  load_row_z<L>(nxt, f, rg.first * C::XR + q, tid);
   __syncthreads();
-  for (int it = 0; it < rg.count; ++it) {
-    const int y0 = (rg.first + it * rg.stride) * C::XR;
-    stage_regs<L, 0, -1>(nxt, tid, twL);
-    lds_write<L, 0>(buf, nxt, tid);
-    if (it + 1 < rg.count) load_row_z<L>(nxt, f, y0 + rg.stride * C::XR + q, tid);
-    __syncthreads();
-    double2 v[16];
-    run_stages<L, 1, -1, true>(buf, v, tid, twL);
-
-    // post-process, two outputs per pair: X[m] = E[m] + W^m O[m], X[L-m] likewise;
-    // slot 0 = X[0] + i X[L]; m = L/2 is its own partner.
-#pragma unroll 1
-    for (int i = 0; i < C::PAIRS; ++i) {
-      int qq, m;
-      pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
-      const double2* bq = lds + qq * P::ROWSTRIDE;
-      const double2 Zm = bq[padx(m)];
-      const int y = y0 + qq;
-      if (m == 0) {
-        H[sidx<TILE>(0, y, M)] = make_double2(Zm.x + Zm.y, Zm.x - Zm.y);
-        const double2 Zh = bq[padx(L / 2)];  // X[L/2] = E + W^{L/2} O, W^{L/2} = -i
-        H[sidx<TILE>(L / 2, y, M)] = make_double2(Zh.x, -Zh.y);
-      } else {
-        const double2 Zp = bq[padx(L - m)];
-        const double2 Zc = cconj(Zp);
-        const double2 E = make_double2(0.5 * (Zm.x + Zc.x), 0.5 * (Zm.y + Zc.y));
-        const double2 D = csub(Zm, Zc);                       // = 2i O[m]
-        const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
-        const double2 WO = cmul(twN.w(m), O);
-        H[sidx<TILE>(m, y, M)] = cadd(E, WO);
-        // X[L-m] = conj(E[m]) + W^{L-m} conj(O[m]) = conj(E[m] - W^m O[m])
-        H[sidx<TILE>(L - m, y, M)] = cconj(csub(E, WO));
-      }
-    }
-    __syncthreads();  // LDS is rewritten by the next item
-  }
+  auto item_y0 = [&](int it) { return (rg.first + it * rg.stride) * C::XR; };
+  rows_fwd_item<L, TILE>(nxt, lds, buf, f, H, M, item_y0(0), rg.count > 1 ? item_y0(1) : -1, q,
+                         tid, twL, twN);
+  for (int it = 1; it < rg.count; ++it)
+    rows_fwd_item<L, TILE>(nxt, lds, buf, f, H, M, item_y0(it),
+                           it + 1 < rg.count ? item_y0(it + 1) : -1, q, tid, twL, twN);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -304,8 +332,59 @@ __device__ __forceinline__ void load_inv(InvLoads<L>& ld, const double2* __restr
     pair_index<L>(tx + i * C::THREADS, qq, m);
     ld.xm[i] = base[(unsigned)sidx<TILE>(m, qq, M)];
     ld.xp[i] = base[(unsigned)sidx<TILE>((L - m) & (L - 1), qq, M)];  // m = 0: unused
-    if (m == 0) ld.xh = base[(unsigned)sidx<TILE>(L / 2, qq, M)];
+    // m = 0 occurs in pair 0 only (later pairs start at m >= 16); every lane loads, the
+    // others a second copy of X[m] that is never used: 17 unconditional loads per item
+    if (i == 0) ld.xh = base[(unsigned)sidx<TILE>(m == 0 ? L / 2 : m, qq, M)];
   }
+}
+
+// One work item (XR rows) of the inverse row pass: c2r pre-processing of the prefetched
+// spectrum pairs into LDS, refill of `nxt` with the next item (next_y0 >= 0), inverse FFT,
+// real rows out.  Branch-free with 17 loads and 16 stores per thread, first item peeled by
+// the kernel: see rows_fwd_item for why (counted vmcnt at the top of an item).
+template <int L, bool TILE>
+__device__ __forceinline__ void rows_inv_item(InvLoads<L>& nxt, double2* lds, double2* buf,
+                                              const double2* __restrict__ H,
+                                              double* __restrict__ f, int M, int y0,
+                                              int next_y0, int q, int tid,
+                                              const TwLds<L>& twL, const TwLds<2 * L>& twN) {
+  using P = Plan<L>;
+  using C = RowCfg<L>;
+#pragma unroll
+  for (int i = 0; i < C::PAIRS; ++i) {
+    int qq, m;
+    pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+    const bool z0 = i == 0 && m == 0;
+    double2* bq = lds + qq * P::ROWSTRIDE;
+    const double2 Xm = nxt.xm[i];
+    const double2 Xp = cconj(nxt.xp[i]);  // conj X[L-m]
+    const double2 S = cadd(Xm, Xp);
+    const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
+    double2 o1 = make_double2(S.x - D.y, S.y + D.x);
+    // Z[L-m] = S' + i D' with S' = conj(S), D' = W^{-(L-m)} (X[L-m] - conj X[m]) = conj(D)
+    double2 o2 = make_double2(S.x + D.y, D.x - S.y);
+    if (i == 0) {
+      if (z0) {  // slot 0 = (X[0], X[L]), both real; Z[L/2] = 2 conj(X[L/2])
+        o1 = make_double2(Xm.x + Xm.y, Xm.x - Xm.y);
+        o2 = make_double2(2.0 * nxt.xh.x, -2.0 * nxt.xh.y);
+      }
+    }
+    bq[padx(m)] = o1;
+    bq[padx(z0 ? L / 2 : L - m)] = o2;
+  }
+  if (next_y0 >= 0) load_inv<L, TILE>(nxt, H, M, next_y0);
+  __syncthreads();
+
+  double2 v[16];
+  run_stages<L, 0, 1, false>(buf, v, tid, twL);
+  constexpr int SL = P::NSTAGES - 1;
+  constexpr int RL = P::radix(SL);
+  double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + q) * (2 * L));
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) z[out_pos<L, SL>(tid, b, r)] = v[b * RL + r];
+  __syncthreads();  // LDS is rewritten by the next item
 }
 
 template <int L, bool TILE>
@@ -326,43 +405,16 @@ __global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_inv_kernel(
   // registers are refilled with the next item while the FFT runs.
   twL.fill(twL_);
   twN.fill(twN_);
+  if (rg.count <= 0) return;
   InvLoads<L> nxt;
-  if (rg.count > 0) load_inv<L, TILE>(nxt, H, M, rg.first * C::XR);
+  load_inv<L, TILE>(nxt, H, M, rg.first * C::XR);
   __syncthreads();
-  for (int it = 0; it < rg.count; ++it) {
-    const int y0 = (rg.first + it * rg.stride) * C::XR;
-#pragma unroll
-    for (int i = 0; i < C::PAIRS; ++i) {
-      int qq, m;
-      pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
-      double2* bq = lds + qq * P::ROWSTRIDE;
-      const double2 Xm = nxt.xm[i];
-      if (m == 0) {  // slot 0 = (X[0], X[L]), both real; Z[L/2] = 2 conj(X[L/2])
-        bq[padx(0)] = make_double2(Xm.x + Xm.y, Xm.x - Xm.y);
-        bq[padx(L / 2)] = make_double2(2.0 * nxt.xh.x, -2.0 * nxt.xh.y);
-      } else {
-        const double2 Xp = cconj(nxt.xp[i]);  // conj X[L-m]
-        const double2 S = cadd(Xm, Xp);
-        const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
-        bq[padx(m)] = make_double2(S.x - D.y, S.y + D.x);
-        // Z[L-m] = S' + i D' with S' = conj(S), D' = W^{-(L-m)} (X[L-m] - conj X[m]) = conj(D)
-        bq[padx(L - m)] = make_double2(S.x + D.y, D.x - S.y);
-      }
-    }
-    if (it + 1 < rg.count) load_inv<L, TILE>(nxt, H, M, y0 + rg.stride * C::XR);
-    __syncthreads();
-
-    double2 v[16];
-    run_stages<L, 0, 1, false>(buf, v, tid, twL);
-    constexpr int SL = P::NSTAGES - 1;
-    constexpr int RL = P::radix(SL);
-    double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + q) * (2 * L));
-#pragma unroll
-    for (int b = 0; b < 16 / RL; ++b)
-#pragma unroll
-      for (int r = 0; r < RL; ++r) z[out_pos<L, SL>(tid, b, r)] = v[b * RL + r];
-    __syncthreads();  // LDS is rewritten by the next item
-  }
+  auto item_y0 = [&](int it) { return (rg.first + it * rg.stride) * C::XR; };
+  rows_inv_item<L, TILE>(nxt, lds, buf, H, f, M, item_y0(0), rg.count > 1 ? item_y0(1) : -1, q,
+                         tid, twL, twN);
+  for (int it = 1; it < rg.count; ++it)
+    rows_inv_item<L, TILE>(nxt, lds, buf, H, f, M, item_y0(it),
+                           it + 1 < rg.count ? item_y0(it + 1) : -1, q, tid, twL, twN);
 }
 
 // Persistent grid: `per_cu` resident workgroups per CU (LDS-limited), a multiple of 8.
