@@ -415,6 +415,11 @@ struct cfdj_cavity {
   double* ext = nullptr;   // extension / psi_ext (2nx x 2ny real)
   double* ext2 = nullptr;  // rocFFT path output
   double2* spec = nullptr;
+  // DST-I on the cavity's own interior (dst_poisson.hip; powers of two 512..4096)
+  bool use_dst = false;
+  double2* dstT = nullptr;
+  double2 *twX = nullptr, *twY = nullptr;
+  int ncu = 256;
   // multigrid alternative
   int poisson = CFDJ_CAVITY_DST;
   Multigrid mg;
@@ -431,7 +436,31 @@ struct cfdj_cavity {
 
   size_t field() const { return (size_t)P * (ny + 1); }
 
+  DstPoissonArgs dst_args(const double* w, double* s) const {
+    DstPoissonArgs a;
+    a.nx = nx;
+    a.ny = ny;
+    a.P = P;
+    a.JT = ny;
+    a.w = w;
+    a.s = s;
+    a.T = dstT;
+    a.tx = sym.cx;
+    a.ty = sym.cy;
+    a.scale = sym.scale;
+    a.neg = true;
+    a.twX = twX;
+    a.twY = twY;
+    a.ncu = ncu;
+    return a;
+  }
+
   void dst_poisson(const double* w, double* s) {  // s_interior = fps_sine(-w)
+    if (use_dst) {
+      const DstPoissonArgs a = dst_args(w, s);
+      for (int pass = 0; pass < 3; ++pass) launch_dst_poisson_pass(pass, a, stream);
+      return;
+    }
     const int NX = 2 * nx, NY = 2 * ny;
     hipLaunchKernelGGL(odd_extend_kernel, dim3((NX + 255) / 256, NY), dim3(256), 0, stream, w,
                        ext, nx, ny, P);
@@ -524,6 +553,9 @@ struct cfdj_cavity {
     dfree(ext);
     dfree(ext2);
     dfree(spec);
+    dfree(dstT);
+    if (twY != twX) dfree(twY);
+    dfree(twX);
     if (mg_ready) mg.destroy();
     dfree(mg_f);
     dfree(part);
@@ -572,6 +604,17 @@ int cfdj_cavity_create(int nx, int ny, double dx, double dy, double re, int devi
     }
     const int NX = 2 * nx, NY = 2 * ny;
     h->sym.init(NX, NY, dx, dy, 0.0, kSymbolDirichletExt);
+    const char* ext_env = std::getenv("CFDJ_CAVITY_EXT");  // A/B: the extension-grid solver
+    if (dst_poisson_supported(nx, ny) && !(ext_env && ext_env[0] == '1')) {
+      h->use_dst = true;
+      h->dstT = dalloc<double2>((size_t)(nx / 2) * ny);
+      h->twX = twiddle_table(NX);
+      h->twY = NY == NX ? h->twX : twiddle_table(NY);
+      CFDJ_HIP(hipDeviceGetAttribute(&h->ncu, hipDeviceAttributeMultiprocessorCount, h->device));
+      h->part = dalloc<double>(cfdj_cavity::kParts);
+      *out = h.release();
+      return;
+    }
     h->ext = dalloc<double>((size_t)NX * NY);
     h->spec = dalloc<double2>((size_t)(NX / 2 + 1) * NY);
     if (fused_ok(NX, NY, 1)) {

@@ -165,6 +165,27 @@ bool fused_poisson_supported(int nx, int ny, int rows);
 bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);
 
+// DST-I Poisson solve of the cavity on its own interior (dst_poisson.hip): pass 0 = x-DST of
+// the rows of w (sign folded in) -> T, pass 1 = y-DST, iden multiply, y-DST on T in place,
+// pass 2 = x-DST of the rows of T -> interior of s.  T holds (nx/2) mode pairs x JT row
+// slots (row j in slot j - 1, JT >= ny); tx / ty are the Dirichlet symbol tables of the
+// (2nx) x (2ny) extension grid (tx[k], k <= nx; ty[p], p < 2ny, even about ny).
+struct DstPoissonArgs {
+  int nx, ny, P, JT;   // cavity cells, node-array pitch, row slots per mode pair
+  const double* w;     // (nx+1) x (ny+1) node array, right-hand side = (neg ? -w : w)
+  double* s;           // node array receiving the interior solution
+  double2* T;
+  const double* tx;
+  const double* ty;
+  double scale;        // 1 / ((2nx)(2ny))
+  bool neg;
+  const double2* twX;  // exp(-2 pi i k / (2nx))
+  const double2* twY;  // exp(-2 pi i k / (2ny))
+  int ncu;
+};
+bool dst_poisson_supported(int nx, int ny);
+void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
+
 // FFT-fused stage kernel (vm_fused.hip): row c2r of the column-pass output HA (rotated
 // layout: row y at (y - 1) mod ny) -> psi in LDS -> Arakawa + RK3 stage -> omega_out (HBM)
 // -> row r2c -> HB (natural layout), one GPU, power-of-two nx 1024..4096, ny 1024..8192.

@@ -1,0 +1,296 @@
+// DST-I Poisson solve of the lid-driven cavity (lid_driven_cavity.jl:11-21 `fps_sine`) on
+// gfx950, on the cavity's own (nx-1) x (ny-1) interior -- three passes over 8 B per cell each
+// way, no 2nx x 2ny extension grid in HBM:
+//
+//   rows_fwd : FFTW's RODFT00 of a row, S[k] = 2 sum_i x_i sin(pi i k / nx), is -Im of the
+//              length-2nx DFT of the row's odd extension.  Two rows a, b ride one complex
+//              transform z = ext(a) + i ext(b): Re Z[k] = S_b[k], -Im Z[k] = S_a[k].  The
+//              extension is built in registers from the nx-1 loaded values; the 2nx-point
+//              Stockham FFT runs in LDS; the coefficients go out as pairs of x-modes,
+//              T[kappa][j] = (S_{2 kappa}[j], S_{2 kappa + 1}[j]), column-major (y
+//              contiguous), so a workgroup's 4 (or more) rows make whole 64-B segments.
+//   cols     : one workgroup per mode pair: its column is a contiguous double2 array whose
+//              two components are two real columns -- again one packed odd-extension
+//              transform (length 2ny), the multiplication by the reference's iden table
+//              (lid_driven_cavity.jl:17,64-69; evaluated as tx[k] + ty[l], reciprocal, as
+//              the periodic path's Dirichlet symbol), and the second DST-I (the same packed
+//              transform: the spectrum of an odd sequence is odd, so the register contents
+//              are already the extended input), 1 / ((2nx)(2ny)) folded in.  In place.
+//   rows_inv : the second x-DST of each row pair from T, real rows out (interior only).
+//
+// Powers of two nx, ny in 512..4096 (FFT lengths 1024..8192); other sizes use the periodic
+// solver on the odd-odd extension (cavity.hip).  FMA contraction is on, as in the periodic
+// FFT passes: the transform is compared with scipy's DST-I at 1e-12 relative.
+#pragma clang fp contract(fast)
+#include "fft_lds.hpp"
+
+namespace cfdj {
+
+namespace {
+
+// Row passes: RP row pairs (2 RP rows) per work item, one packed FFT of length M2 each.
+template <int M2>
+struct DstRowCfg {
+  static constexpr int T = Plan<M2>::T;
+  static constexpr int RP = 8192 / M2 < 1 ? 1 : 8192 / M2;  // 139 KB of LDS
+  static constexpr int ROWS = 2 * RP;
+  static constexpr int THREADS = RP * T;
+  static constexpr int ENTRIES = (M2 / 4) * ROWS / THREADS;  // (mode pair, row) per thread
+  static_assert(ENTRIES == 8, "entry mapping");
+};
+
+// Entry e of a work item: row rr of the item, mode pair kappa.  16 consecutive lanes take
+// 16 consecutive mode pairs of one row; ROWS consecutive 16-lane groups take the item's
+// rows, so a wave's global accesses cover whole ROWS*16-B segments per mode pair.
+template <int M2>
+__device__ __forceinline__ void entry_index(int e, int& rr, int& kap) {
+  using C = DstRowCfg<M2>;
+  rr = (e >> 4) % C::ROWS;
+  kap = ((e >> 4) / C::ROWS) * 16 + (e & 15);
+}
+
+// Stage-0 registers of the packed odd extension of rows ja (real part) and ja + 1
+// (imaginary part) of the node array w (pitch P); rows beyond ny - 1 count as zero; sgn
+// folds the reference's f = -w.
+template <int M2>
+__device__ __forceinline__ void load_row_pair(double2 (&v)[16], const double* __restrict__ w,
+                                              int P, int ny, int ja, int tid, double sgn) {
+  constexpr int nx = M2 / 2;
+  constexpr int R0 = Plan<M2>::radix(0);
+  const bool oka = ja <= ny - 1, okb = ja + 1 <= ny - 1;
+  const double* ra = w + (size_t)(oka ? ja : 1) * P;
+  const double* rb = w + (size_t)(okb ? ja + 1 : 1) * P;
+#pragma unroll
+  for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+    for (int r = 0; r < R0; ++r) {
+      const int p = in_pos<M2, 0>(tid, b, r);
+      const int i = p < nx ? p : M2 - p;          // mirrored node, 1..nx-1 (or 0 / nx)
+      const bool zero = (p & (nx - 1)) == 0;      // p == 0 or p == nx
+      const double s = p < nx ? sgn : -sgn;
+      const int ii = zero ? 1 : i;
+      const double a = ra[ii], bq = rb[ii];
+      v[b * R0 + r] = make_double2(zero || !oka ? 0.0 : s * a, zero || !okb ? 0.0 : s * bq);
+    }
+}
+
+template <int M2>
+__global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_fwd_kernel(
+    const double* __restrict__ w, int P, int ny, double2* __restrict__ T, int JT, double sgn,
+    const double2* __restrict__ tw_) {
+  using PL = Plan<M2>;
+  using C = DstRowCfg<M2>;
+  __shared__ double2 lds[C::RP * PL::PAD];
+  __shared__ TwLds<M2> tw;
+  const int q = threadIdx.x / PL::T;
+  const int tid = threadIdx.x % PL::T;
+  double2* buf = lds + q * PL::PAD;
+  const Range rg = persistent_range(blockIdx.x, gridDim.x, ny / C::ROWS);
+  tw.fill(tw_);
+  if (rg.count <= 0) return;
+  double2 nxt[16];
+  load_row_pair<M2>(nxt, w, P, ny, 1 + rg.first * C::ROWS + 2 * q, tid, sgn);
+  __syncthreads();
+  for (int it = 0; it < rg.count; ++it) {
+    const int slot0 = (rg.first + it * rg.stride) * C::ROWS;  // row j lives in slot j - 1
+    stage_regs<M2, 0, -1>(nxt, tid, tw);
+    lds_write<M2, 0>(buf, nxt, tid);
+    if (it + 1 < rg.count)
+      load_row_pair<M2>(nxt, w, P, ny, 1 + slot0 + rg.stride * C::ROWS + 2 * q, tid, sgn);
+    __syncthreads();
+    double2 v[16];
+    run_stages<M2, 1, -1, true>(buf, v, tid, tw);
+    double2* tb = T + __builtin_amdgcn_readfirstlane(slot0);
+#pragma unroll
+    for (int i = 0; i < C::ENTRIES; ++i) {
+      int rr, kap;
+      entry_index<M2>(threadIdx.x + i * C::THREADS, rr, kap);
+      const double2* bq = lds + (rr >> 1) * PL::PAD;
+      const double2 Z0 = bq[padx(2 * kap)];
+      const double2 Z1 = bq[padx(2 * kap + 1)];
+      // first row of the pair: -Im Z; second row: Re Z
+      const double2 o = (rr & 1) ? make_double2(Z0.x, Z1.x) : make_double2(-Z0.y, -Z1.y);
+      tb[(unsigned)(kap * JT + rr)] = o;
+    }
+    __syncthreads();  // LDS is rewritten by the next item
+  }
+}
+
+template <int M2>
+__global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
+    const double2* __restrict__ T, int JT, double* __restrict__ s, int P, int ny,
+    const double2* __restrict__ tw_) {
+  using PL = Plan<M2>;
+  using C = DstRowCfg<M2>;
+  constexpr int nx = M2 / 2;
+  __shared__ double2 lds[C::RP * PL::PAD];
+  __shared__ TwLds<M2> tw;
+  const int q = threadIdx.x / PL::T;
+  const int tid = threadIdx.x % PL::T;
+  double2* buf = lds + q * PL::PAD;
+  const Range rg = persistent_range(blockIdx.x, gridDim.x, ny / C::ROWS);
+  tw.fill(tw_);
+  if (rg.count <= 0) return;
+  auto load_entries = [&](double2 (&e)[C::ENTRIES], int slot0) {
+    const double2* tb = T + __builtin_amdgcn_readfirstlane(slot0);
+    int tx = threadIdx.x;
+    asm volatile("" : "+v"(tx));  // keep the 8 offsets out of loop-invariant registers
+#pragma unroll
+    for (int i = 0; i < C::ENTRIES; ++i) {
+      int rr, kap;
+      entry_index<M2>(tx + i * C::THREADS, rr, kap);
+      e[i] = tb[(unsigned)(kap * JT + rr)];
+    }
+  };
+  double2 nxt[C::ENTRIES];
+  load_entries(nxt, rg.first * C::ROWS);
+  __syncthreads();
+  for (int it = 0; it < rg.count; ++it) {
+    const int slot0 = (rg.first + it * rg.stride) * C::ROWS;
+    // entries -> packed odd extension in LDS: row parity picks the real / imaginary part,
+    // mode k goes to p = k and, negated, to p = 2nx - k; p = 0 and p = nx are zero.
+#pragma unroll
+    for (int i = 0; i < C::ENTRIES; ++i) {
+      int rr, kap;
+      entry_index<M2>(threadIdx.x + i * C::THREADS, rr, kap);
+      double* bq = reinterpret_cast<double*>(lds + (rr >> 1) * PL::PAD) + (rr & 1);
+      const int k0 = 2 * kap, k1 = k0 + 1;
+      const double v0 = k0 == 0 ? 0.0 : nxt[i].x;  // mode 0 of a sine series does not exist
+      bq[2 * padx(k0)] = v0;
+      bq[2 * padx(k1)] = nxt[i].y;
+      if (k0 != 0) bq[2 * padx(M2 - k0)] = -v0;
+      else bq[2 * padx(nx)] = 0.0;  // the kappa = 0 lanes also clear p = nx
+      bq[2 * padx(M2 - k1)] = -nxt[i].y;
+    }
+    if (it + 1 < rg.count) load_entries(nxt, slot0 + rg.stride * C::ROWS);
+    __syncthreads();
+    double2 v[16];
+    run_stages<M2, 0, -1, false>(buf, v, tid, tw);
+    constexpr int SL = PL::NSTAGES - 1;
+    constexpr int RL = PL::radix(SL);
+    const int ja = 1 + slot0 + 2 * q;
+    const bool oka = ja <= ny - 1, okb = ja + 1 <= ny - 1;
+    double* sa = s + (size_t)ja * P;
+    double* sb = sa + P;
+#pragma unroll
+    for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        const int p = out_pos<M2, SL>(tid, b, r);
+        if (p >= 1 && p < nx) {
+          if (oka) sa[p] = -v[b * RL + r].y;
+          if (okb) sb[p] = v[b * RL + r].x;
+        }
+      }
+    __syncthreads();  // LDS is rewritten by the next item
+  }
+}
+
+// One mode pair per workgroup: packed y-DST, times iden, packed y-DST, in place.
+template <int M2>
+__global__ __launch_bounds__(Plan<M2>::T) void dst_cols_kernel(double2* __restrict__ T, int JT,
+                                                             const double* __restrict__ tx,
+                                                             const double* __restrict__ ty,
+                                                             double scale,
+                                                             const double2* __restrict__ tw_) {
+  using PL = Plan<M2>;
+  static_assert(PL::NSTAGES >= 2, "column length");
+  constexpr int ny = M2 / 2;
+  __shared__ double2 lds[PL::PAD];
+  const TwGlobal<M2> tw{tw_};
+  const int tid = threadIdx.x;
+  const int kap = xcd_remap(blockIdx.x, gridDim.x);
+  double2* col = T + (size_t)kap * JT;  // row j in slot j - 1
+
+  double2 a[16];
+  constexpr int R0 = PL::radix(0);
+#pragma unroll
+  for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+    for (int r = 0; r < R0; ++r) {
+      const int p = in_pos<M2, 0>(tid, b, r);
+      const bool zero = (p & (ny - 1)) == 0;
+      const int j = p < ny ? p : M2 - p;
+      const double2 c = col[zero ? 0 : j - 1];
+      const double s = p < ny ? 1.0 : -1.0;
+      a[b * R0 + r] = zero ? make_double2(0.0, 0.0) : make_double2(s * c.x, s * c.y);
+    }
+  stage_regs<M2, 0, -1>(a, tid, tw);
+  lds_write<M2, 0>(lds, a, tid);
+  __syncthreads();
+  run_stages<M2, 1, -1, false>(lds, a, tid, tw);  // last stage stays in registers
+
+  double2 v[16];
+  fwd_to_inv<M2>(a, v);  // v[r] = Z[p], p = tid + T r
+  const double txa = tx[2 * kap], txb = tx[2 * kap + 1];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int p = tid + PL::T * r;
+    const bool zero = (p & (ny - 1)) == 0;
+    const double t = ty[p];  // even in p about ny (the table holds the extension)
+    // S_a = -Im Z, S_b = Re Z; times iden (lid_driven_cavity.jl:17), then the second
+    // transform's input ext(S_a iden_a) + i ext(S_b iden_b): the oddness is already there
+    const double ia = recip_nr(fd_symbol(txa, 1.0, t));
+    const double ib = recip_nr(fd_symbol(txb, 1.0, t));
+    const double2 z = make_double2((-v[r].y * ia) * scale, (v[r].x * ib) * scale);
+    v[r] = zero ? make_double2(0.0, 0.0) : z;
+  }
+  __syncthreads();  // LDS is rewritten by the second transform's stage 0
+  stage_regs<M2, 0, -1>(v, tid, tw);
+  lds_write<M2, 0>(lds, v, tid);
+  __syncthreads();
+  run_stages<M2, 1, -1, false>(lds, v, tid, tw);
+  constexpr int SL = PL::NSTAGES - 1;
+  constexpr int RL = PL::radix(SL);
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) {
+      const int p = out_pos<M2, SL>(tid, b, r);
+      if (p >= 1 && p < ny) col[p - 1] = make_double2(-v[b * RL + r].y, v[b * RL + r].x);
+    }
+}
+
+template <int M2>
+void launch_dst_rows(int pass, const DstPoissonArgs& a, hipStream_t st) {
+  using C = DstRowCfg<M2>;
+  int nb = a.ncu - a.ncu % 8;
+  if (nb < 8) nb = 8;
+  const int items = a.ny / C::ROWS;
+  const dim3 grid(nb < items ? nb : items);
+  if (pass == 0)
+    hipLaunchKernelGGL((dst_rows_fwd_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.w, a.P, a.ny,
+                       a.T, a.JT, a.neg ? -1.0 : 1.0, a.twX);
+  else
+    hipLaunchKernelGGL((dst_rows_inv_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.T, a.JT, a.s,
+                       a.P, a.ny, a.twX);
+}
+
+template <int M2>
+void launch_dst_cols(const DstPoissonArgs& a, hipStream_t st) {
+  hipLaunchKernelGGL((dst_cols_kernel<M2>), dim3(a.nx / 2), dim3(Plan<M2>::T), 0, st, a.T, a.JT,
+                     a.tx, a.ty, a.scale, a.twY);
+}
+
+constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
+
+}  // namespace
+
+bool dst_poisson_supported(int nx, int ny) {
+  return pow2(nx) && pow2(ny) && nx >= 512 && nx <= 4096 && ny >= 512 && ny <= 4096;
+}
+
+void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st) {
+  if (!dst_poisson_supported(a.nx, a.ny) || a.JT < a.ny || a.P < a.nx + 1)
+    throw Error{CFDJ_ERR_ARG, "DST Poisson: unsupported size"};
+  const int n = pass == 1 ? a.ny : a.nx;
+  switch (2 * n) {
+    case 1024: pass == 1 ? launch_dst_cols<1024>(a, st) : launch_dst_rows<1024>(pass, a, st); break;
+    case 2048: pass == 1 ? launch_dst_cols<2048>(a, st) : launch_dst_rows<2048>(pass, a, st); break;
+    case 4096: pass == 1 ? launch_dst_cols<4096>(a, st) : launch_dst_rows<4096>(pass, a, st); break;
+    default: pass == 1 ? launch_dst_cols<8192>(a, st) : launch_dst_rows<8192>(pass, a, st); break;
+  }
+  CFDJ_HIP(hipGetLastError());
+}
+
+}  // namespace cfdj

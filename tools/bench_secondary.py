@@ -129,10 +129,17 @@ def bench_slabs(steps=3):
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--only", default="poisson,cavity,spectral,slabs",
+                    help="comma-separated sections: poisson, cavity, spectral, slabs")
     a = ap.parse_args()
-    print(json.dumps(bench_poisson()))
-    print(json.dumps(bench_cavity(steps=a.steps)))
-    for r in bench_spectral():
-        print(json.dumps(r))
-    for r in bench_slabs():
-        print(json.dumps(r))
+    only = set(a.only.split(","))
+    if "poisson" in only:
+        print(json.dumps(bench_poisson()), flush=True)
+    if "cavity" in only:
+        print(json.dumps(bench_cavity(steps=a.steps)), flush=True)
+    if "spectral" in only:
+        for r in bench_spectral():
+            print(json.dumps(r), flush=True)
+    if "slabs" in only:
+        for r in bench_slabs():
+            print(json.dumps(r), flush=True)
