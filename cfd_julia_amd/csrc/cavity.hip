@@ -149,24 +149,6 @@ __global__ __launch_bounds__(256) void sumsq_final_kernel(const double* __restri
   if (threadIdx.x == 0) *out = sqrt(red[0] / denom);
 }
 
-// ---- multigrid (Common.jl) ------------------------------------------------------------
-// One red-black half sweep of the Common.jl:84-88 update on points with (i + j) % 2 ==
-// parity (the reference's lexicographic order is inherently serial; converged solutions
-// agree to the solver tolerance, tests/test_gpu_cavity.py).
-__global__ __launch_bounds__(kBX* kBY) void rbgs_kernel(const double* __restrict__ f,
-                                                        double* __restrict__ u, int nx, int ny,
-                                                        int P, double dx2, double dy2,
-                                                        double dd, int parity) {
-  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
-  const int i = 1 + 2 * (blockIdx.x * kBX + threadIdx.x) + ((j + 1 + parity) & 1);
-  if (i >= nx || j >= ny) return;
-  const size_t c = (size_t)j * P + i;
-  const double uc = u[c];
-  const double rt = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 +
-                            (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
-  u[c] = uc + rt / dd;
-}
-
 // Common.jl:239-246
 __global__ __launch_bounds__(kBX* kBY) void residual_kernel(const double* __restrict__ f,
                                                             const double* __restrict__ u,
@@ -179,52 +161,6 @@ __global__ __launch_bounds__(kBX* kBY) void residual_kernel(const double* __rest
   const size_t c = (size_t)j * P + i;
   const double uc = u[c];
   r[c] = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 + (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
-}
-
-// Common.jl:21-48: full weighting on the coarse interior, injection on its boundary.
-__global__ __launch_bounds__(kBX* kBY) void restriction_kernel(const double* __restrict__ r,
-                                                               double* __restrict__ ec, int nxf,
-                                                               int nyf, int Pf, int nxc,
-                                                               int nyc, int Pc) {
-  const int i = blockIdx.x * kBX + threadIdx.x;  // 0..nxc
-  const int j = blockIdx.y * kBY + threadIdx.y;  // 0..nyc
-  if (i > nxc || j > nyc) return;
-  double v;
-  if (i == 0 || i == nxc || j == 0 || j == nyc) {
-    // the reference's boundary loops: bottom/top (i = 1, nxc+1: rows of r) run first, then
-    // left/right (j = 1, nyc+1) overwrite the corners -- both inject the same node
-    v = r[(size_t)(j == 0 ? 0 : (j == nyc ? nyf : 2 * j)) * Pf +
-          (i == 0 ? 0 : (i == nxc ? nxf : 2 * i))];
-  } else {
-    const size_t c = (size_t)(2 * j) * Pf + 2 * i;
-    const double center = 4.0 * r[c];
-    const double grid = 2.0 * (r[c + Pf] + r[c - Pf] + r[c + 1] + r[c - 1]);
-    const double corner = r[c + Pf + 1] + r[c - Pf + 1] + r[c + Pf - 1] + r[c - Pf - 1];
-    v = (center + grid + corner) / 16.0;
-  }
-  ec[(size_t)j * Pc + i] = v;
-}
-
-// Common.jl:50-76 + mg_N.jl:99-101: u_f[interior] += bilinear prolongation of u_c.
-__global__ __launch_bounds__(kBX* kBY) void prolong_add_kernel(const double* __restrict__ uc,
-                                                               double* __restrict__ uf, int nxf,
-                                                               int nyf, int Pf, int Pc) {
-  const int I = 1 + blockIdx.x * kBX + threadIdx.x;
-  const int J = 1 + blockIdx.y * kBY + threadIdx.y;
-  if (I >= nxf || J >= nyf) return;
-  const int ic = I >> 1, jc = J >> 1;
-  const size_t c = (size_t)jc * Pc + ic;
-  double p;
-  if (!(I & 1) && !(J & 1)) {
-    p = uc[c];
-  } else if (!(I & 1)) {  // J odd: ef[2i-1, 2j] = .5(unc[i,j] + unc[i,j+1])
-    p = 0.5 * (uc[c] + uc[c + Pc]);
-  } else if (!(J & 1)) {  // I odd: ef[2i, 2j-1] = .5(unc[i,j] + unc[i+1,j])
-    p = 0.5 * (uc[c] + uc[c + 1]);
-  } else {
-    p = 0.25 * (uc[c] + uc[c + Pc] + uc[c + 1] + uc[c + Pc + 1]);
-  }
-  uf[(size_t)J * Pf + I] += p;
 }
 
 // 15_Poisson_Solver_Gauss_Seidel/gauss_seidel.jl:33-39 (a Jacobi sweep despite the name):
@@ -256,6 +192,325 @@ dim3 interior_grid(int nx, int ny) {
   return dim3((nx - 1 + kBX - 1) / kBX, (ny - 1 + kBY - 1) / kBY);
 }
 
+// ---- multigrid V-cycle kernels (device-resident convergence control) -------------------
+// ctl[0] = converged flag, ctl[1] = number of residual norms recorded so far (hist index).
+// Every kernel of a cycle returns at once when the flag is set, so cycles enqueued past the
+// converged one (the host enqueues whole cycles without reading the norm back) change
+// nothing: the iterate stays the one mg_N.jl:70 breaks on.
+__device__ __forceinline__ bool mg_done(const int* ctl) { return ctl != nullptr && ctl[0] != 0; }
+
+// One red-black half sweep of the Common.jl:84-88 update on points with (i + j) % 2 ==
+// parity (the reference's lexicographic order is inherently serial; converged solutions
+// agree to the solver tolerance, tests/test_gpu_cavity.py).
+__global__ __launch_bounds__(kBX* kBY) void mg_rbgs_kernel(const double* __restrict__ f,
+                                                           double* __restrict__ u, int nx, int ny,
+                                                           int P, double dx2, double dy2,
+                                                           double dd, int parity,
+                                                           const int* __restrict__ ctl) {
+  if (mg_done(ctl)) return;
+  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
+  const int i = 1 + 2 * (blockIdx.x * kBX + threadIdx.x) + ((j + 1 + parity) & 1);
+  if (i >= nx || j >= ny) return;
+  const size_t c = (size_t)j * P + i;
+  const double uc = u[c];
+  const double rt = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 +
+                            (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
+  u[c] = uc + rt / dd;
+}
+
+// S full red-black sweeps (2S half sweeps) of the same update in ONE pass over the level:
+// a workgroup loads its 64 x 32 tile of u and f plus a halo of 2S nodes into LDS, runs the
+// half sweeps there (each one valid on a region one node smaller all round: an update needs
+// its four neighbours' values of the previous half sweep), and writes the tile to `uout`.
+// Every point of the tile sees exactly the neighbour values the separate half-sweep
+// launches would give it, so the result is bit-identical to them; HBM traffic per call is
+// f + u in + u out (24 B per node) instead of 2S x (f + u + u).  Out of place: neighbouring
+// tiles read each other's old values (the caller ping-pongs the two buffers).
+constexpr int kFsTX = 64, kFsTY = 32;
+template <int S>
+__global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __restrict__ f,
+                                                              const double* __restrict__ uin,
+                                                              double* __restrict__ uout, int nx,
+                                                              int ny, int P, double dx2,
+                                                              double dy2, double dd,
+                                                              const int* __restrict__ ctl) {
+  if (mg_done(ctl)) return;
+  constexpr int H = 2 * S, W = kFsTX + 2 * H, HT = kFsTY + 2 * H;
+  __shared__ double su[HT * W];
+  __shared__ double sf[HT * W];
+  const int x0 = blockIdx.x * kFsTX - H, y0 = blockIdx.y * kFsTY - H;  // node of local (0, 0)
+  for (int e = threadIdx.x; e < W * HT; e += 256) {
+    const int lj = e / W, li = e % W;
+    const int gi = x0 + li, gj = y0 + lj;
+    double uv = 0.0, fv = 0.0;
+    if (gi >= 0 && gi <= nx && gj >= 0 && gj <= ny) {
+      const size_t c = (size_t)gj * P + gi;
+      uv = uin[c];
+      fv = f[c];
+    }
+    su[e] = uv;
+    sf[e] = fv;
+  }
+  __syncthreads();
+#pragma unroll 1
+  for (int h = 1; h <= 2 * S; ++h) {
+    const int parity = (h - 1) & 1;
+    const int wdt = W - 2 * h, hgt = HT - 2 * h;  // local region [h, W-1-h] x [h, HT-1-h]
+    const int hw = (wdt + 1) / 2;
+    for (int e = threadIdx.x; e < hw * hgt; e += 256) {
+      const int lj = h + e / hw;
+      const int gj = y0 + lj;
+      // first local column >= h whose node has (gi + gj) % 2 == parity
+      const int li = h + 2 * (e % hw) + ((x0 + h + gj + parity) & 1);
+      const int gi = x0 + li;
+      if (li <= W - 1 - h && gi >= 1 && gi < nx && gj >= 1 && gj < ny) {
+        const int c = lj * W + li;
+        const double uc = su[c];
+        const double rt = sf[c] - ((su[c + 1] - 2.0 * uc + su[c - 1]) / dx2 +
+                                   (su[c + W] - 2.0 * uc + su[c - W]) / dy2);
+        su[c] = uc + rt / dd;
+      }
+    }
+    __syncthreads();
+  }
+  for (int e = threadIdx.x; e < kFsTX * kFsTY; e += 256) {
+    const int lj = H + e / kFsTX, li = H + e % kFsTX;
+    const int gi = x0 + li, gj = y0 + lj;
+    if (gi <= nx && gj <= ny) uout[(size_t)gj * P + gi] = su[lj * W + li];
+  }
+}
+
+// Common.jl:239-246 residual; with part != nullptr also this block's sum of r^2 (fixed
+// in-block order: the norm of Common.jl:229-232 without a second pass over r).
+__global__ __launch_bounds__(kBX* kBY) void mg_residual_kernel(const double* __restrict__ f,
+                                                               const double* __restrict__ u,
+                                                               double* __restrict__ r, int nx,
+                                                               int ny, int P, double dx2,
+                                                               double dy2,
+                                                               double* __restrict__ part,
+                                                               const int* __restrict__ ctl) {
+  if (mg_done(ctl)) return;
+  __shared__ double red[kBX * kBY];
+  const int i = 1 + blockIdx.x * kBX + threadIdx.x;
+  const int j = 1 + blockIdx.y * kBY + threadIdx.y;
+  double rc = 0.0;
+  if (i < nx && j < ny) {
+    const size_t c = (size_t)j * P + i;
+    const double uc = u[c];
+    rc = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 + (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
+    r[c] = rc;
+  }
+  if (part == nullptr) return;
+  const int t = threadIdx.y * kBX + threadIdx.x;
+  red[t] = rc * rc;
+  __syncthreads();
+  for (int off = kBX * kBY / 2; off > 0; off >>= 1) {
+    if (t < off) red[t] += red[t + off];
+    __syncthreads();
+  }
+  if (t == 0) part[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+}
+
+// rms = sqrt(sum of the block partials / denom) -> hist[ctl[1]++]; first = 1: the initial
+// residual (mg_N.jl:22, no test); else the convergence test of mg_N.jl:70 against hist[0].
+__global__ __launch_bounds__(256) void mg_norm_kernel(const double* __restrict__ part,
+                                                      int nparts, double denom,
+                                                      double* __restrict__ hist, int hist_cap,
+                                                      int* __restrict__ ctl, double tol,
+                                                      int first) {
+  if (mg_done(ctl)) return;
+  __shared__ double red[256];
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
+  red[threadIdx.x] = acc;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const double rms = sqrt(red[0] / denom);
+    const int idx = ctl[1];
+    if (idx < hist_cap) hist[idx] = rms;
+    ctl[1] = idx + 1;
+    if (first) ctl[2] = 0;
+    if (!first && !(rms / hist[0] > tol)) ctl[0] = 1;  // also stops on hist[0] == 0
+  }
+}
+
+// Common.jl:21-48: full weighting on the coarse interior, injection on its boundary (the
+// reference's bottom/top loops run first, then left/right overwrite the corners -- both
+// inject the same node); mg_N.jl:88: the coarse iterate starts at zero.
+__global__ __launch_bounds__(kBX* kBY) void mg_restrict_kernel(const double* __restrict__ r,
+                                                               double* __restrict__ ec,
+                                                               double* __restrict__ uc, int nxf,
+                                                               int nyf, int Pf, int nxc, int nyc,
+                                                               int Pc,
+                                                               const int* __restrict__ ctl) {
+  if (mg_done(ctl)) return;
+  const int i = blockIdx.x * kBX + threadIdx.x;  // 0..nxc
+  const int j = blockIdx.y * kBY + threadIdx.y;  // 0..nyc
+  if (i > nxc || j > nyc) return;
+  double v;
+  if (i == 0 || i == nxc || j == 0 || j == nyc) {
+    v = r[(size_t)(j == 0 ? 0 : (j == nyc ? nyf : 2 * j)) * Pf +
+          (i == 0 ? 0 : (i == nxc ? nxf : 2 * i))];
+  } else {
+    const size_t c = (size_t)(2 * j) * Pf + 2 * i;
+    const double center = 4.0 * r[c];
+    const double grid = 2.0 * (r[c + Pf] + r[c - Pf] + r[c + 1] + r[c - 1]);
+    const double corner = r[c + Pf + 1] + r[c - Pf + 1] + r[c + Pf - 1] + r[c - Pf - 1];
+    v = (center + grid + corner) / 16.0;
+  }
+  ec[(size_t)j * Pc + i] = v;
+  uc[(size_t)j * Pc + i] = 0.0;
+}
+
+// Common.jl:50-76 + mg_N.jl:99-101: u_f[interior] += bilinear prolongation of u_c
+// (even/even: injection; one index odd: mean of 2; both odd: mean of 4).
+__global__ __launch_bounds__(kBX* kBY) void mg_prolong_add_kernel(const double* __restrict__ uc,
+                                                                  double* __restrict__ uf,
+                                                                  int nxf, int nyf, int Pf,
+                                                                  int Pc,
+                                                                  const int* __restrict__ ctl) {
+  if (mg_done(ctl)) return;
+  const int I = 1 + blockIdx.x * kBX + threadIdx.x;
+  const int J = 1 + blockIdx.y * kBY + threadIdx.y;
+  if (I >= nxf || J >= nyf) return;
+  const int ic = I >> 1, jc = J >> 1;
+  const size_t c = (size_t)jc * Pc + ic;
+  double p;
+  if (!(I & 1) && !(J & 1)) {
+    p = uc[c];
+  } else if (!(I & 1)) {
+    p = 0.5 * (uc[c] + uc[c + Pc]);
+  } else if (!(J & 1)) {
+    p = 0.5 * (uc[c] + uc[c + 1]);
+  } else {
+    p = 0.25 * (uc[c] + uc[c + Pc] + uc[c + 1] + uc[c + Pc + 1]);
+  }
+  uf[(size_t)J * Pf + I] += p;
+}
+
+// The coarse levels of a V-cycle (grids of at most 64 cells a side) in ONE workgroup with
+// every level's u and f in LDS: descent from the residual of the finest LDS level's parent
+// (global memory) to the coarsest grid and the ascent back, the same kernels' arithmetic
+// point for point (red-black half sweeps separated by barriers), so the iterates are
+// identical to the level-by-level launches -- which cost a dozen launches of a few hundred
+// threads per level.
+constexpr int kMgCoarseMaxLevels = 8;
+constexpr int kMgCoarseCells = 64;
+struct MgCoarseArgs {
+  int n;                              // coarse levels held in LDS
+  int lnx[kMgCoarseMaxLevels], lny[kMgCoarseMaxLevels], lP[kMgCoarseMaxLevels];
+  double dx2[kMgCoarseMaxLevels], dy2[kMgCoarseMaxLevels], dd[kMgCoarseMaxLevels];
+  int off_u[kMgCoarseMaxLevels], off_f[kMgCoarseMaxLevels], off_r;  // in doubles
+  int sweeps_down[kMgCoarseMaxLevels];  // v1, or v2 on the coarsest level (mg_N.jl:91)
+  int v3;
+  const double* r_in;  // residual of the parent level (global)
+  int nxf, nyf, Pf;    // parent level
+  double* u_out;       // level 0 of the LDS levels, written back for the parent's correction
+  const int* ctl;
+};
+
+__device__ __forceinline__ void lds_smooth(const double* f, double* u, int nx, int ny, int P,
+                                           double dx2, double dy2, double dd, int sweeps) {
+  const int hw = (nx + 1) / 2;
+  const int total = (ny - 1) * hw;
+  for (int s = 0; s < sweeps; ++s)
+    for (int parity = 0; parity < 2; ++parity) {
+      for (int e = threadIdx.x; e < total; e += blockDim.x) {
+        const int j = 1 + e / hw;
+        const int i = 1 + 2 * (e % hw) + ((j + 1 + parity) & 1);
+        if (i < nx) {
+          const int c = j * P + i;
+          const double uc = u[c];
+          const double rt = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 +
+                                    (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
+          u[c] = uc + rt / dd;
+        }
+      }
+      __syncthreads();
+    }
+}
+
+// restriction of a fine residual (any memory) into LDS f, u = 0
+__device__ __forceinline__ void lds_restrict(const double* r, int nxf, int nyf, int Pf, double* ec,
+                                             double* uc, int nxc, int nyc, int Pc) {
+  const int total = (nxc + 1) * (nyc + 1);
+  for (int e = threadIdx.x; e < total; e += blockDim.x) {
+    const int j = e / (nxc + 1), i = e % (nxc + 1);
+    double v;
+    if (i == 0 || i == nxc || j == 0 || j == nyc) {
+      v = r[(size_t)(j == 0 ? 0 : (j == nyc ? nyf : 2 * j)) * Pf +
+            (i == 0 ? 0 : (i == nxc ? nxf : 2 * i))];
+    } else {
+      const size_t c = (size_t)(2 * j) * Pf + 2 * i;
+      const double center = 4.0 * r[c];
+      const double grid = 2.0 * (r[c + Pf] + r[c - Pf] + r[c + 1] + r[c - 1]);
+      const double corner = r[c + Pf + 1] + r[c - Pf + 1] + r[c + Pf - 1] + r[c - Pf - 1];
+      v = (center + grid + corner) / 16.0;
+    }
+    ec[j * Pc + i] = v;
+    uc[j * Pc + i] = 0.0;
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(1024) void mg_coarse_kernel(const MgCoarseArgs a) {
+  if (mg_done(a.ctl)) return;
+  extern __shared__ double sm[];
+  double* rb = sm + a.off_r;
+  // descent
+  lds_restrict(a.r_in, a.nxf, a.nyf, a.Pf, sm + a.off_f[0], sm + a.off_u[0], a.lnx[0], a.lny[0],
+               a.lP[0]);
+  lds_smooth(sm + a.off_f[0], sm + a.off_u[0], a.lnx[0], a.lny[0], a.lP[0], a.dx2[0], a.dy2[0],
+             a.dd[0], a.sweeps_down[0]);
+  for (int c = 1; c < a.n; ++c) {
+    // residual of level c-1 (Common.jl:239-246), boundary entries zero
+    const int nx = a.lnx[c - 1], ny = a.lny[c - 1], P = a.lP[c - 1];
+    const double* f = sm + a.off_f[c - 1];
+    const double* u = sm + a.off_u[c - 1];
+    for (int e = threadIdx.x; e < (nx + 1) * (ny + 1); e += blockDim.x) {
+      const int j = e / (nx + 1), i = e % (nx + 1);
+      double rc = 0.0;
+      if (i >= 1 && i < nx && j >= 1 && j < ny) {
+        const int q = j * P + i;
+        const double uc = u[q];
+        rc = f[q] - ((u[q + 1] - 2.0 * uc + u[q - 1]) / a.dx2[c - 1] +
+                     (u[q + P] - 2.0 * uc + u[q - P]) / a.dy2[c - 1]);
+      }
+      rb[j * P + i] = rc;
+    }
+    __syncthreads();
+    lds_restrict(rb, nx, ny, P, sm + a.off_f[c], sm + a.off_u[c], a.lnx[c], a.lny[c], a.lP[c]);
+    lds_smooth(sm + a.off_f[c], sm + a.off_u[c], a.lnx[c], a.lny[c], a.lP[c], a.dx2[c], a.dy2[c],
+               a.dd[c], a.sweeps_down[c]);
+  }
+  // ascent
+  for (int c = a.n - 1; c >= 1; --c) {
+    const int nxf = a.lnx[c - 1], nyf = a.lny[c - 1], Pf = a.lP[c - 1], Pc = a.lP[c];
+    const double* uc = sm + a.off_u[c];
+    double* uf = sm + a.off_u[c - 1];
+    const int wdt = nxf - 1;
+    for (int e = threadIdx.x; e < wdt * (nyf - 1); e += blockDim.x) {
+      const int J = 1 + e / wdt, I = 1 + e % wdt;
+      const int q = (J >> 1) * Pc + (I >> 1);
+      double p;
+      if (!(I & 1) && !(J & 1)) p = uc[q];
+      else if (!(I & 1)) p = 0.5 * (uc[q] + uc[q + Pc]);
+      else if (!(J & 1)) p = 0.5 * (uc[q] + uc[q + 1]);
+      else p = 0.25 * (uc[q] + uc[q + Pc] + uc[q + 1] + uc[q + Pc + 1]);
+      uf[J * Pf + I] += p;
+    }
+    __syncthreads();
+    lds_smooth(sm + a.off_f[c - 1], uf, nxf, nyf, Pf, a.dx2[c - 1], a.dy2[c - 1], a.dd[c - 1],
+               a.v3);
+  }
+  const double* u0 = sm + a.off_u[0];
+  for (int e = threadIdx.x; e < a.lP[0] * (a.lny[0] + 1); e += blockDim.x) a.u_out[e] = u0[e];
+}
+
 }  // namespace
 
 // ---- host objects ----------------------------------------------------------------------
@@ -268,15 +523,33 @@ static void launch_rms(const double* a, const double* b, int i0, int n0, int j0,
   CFDJ_HIP(hipGetLastError());
 }
 
-// n-level V-cycle (mg_N.jl:7-114) on device buffers.
+// n-level V-cycle (mg_N.jl:7-114) on device buffers.  The convergence test runs on the
+// device (mg_norm_kernel); the host enqueues whole cycles -- one HIP graph replay each --
+// and reads the control words back once per batch: as many cycles as the previous solve
+// took (time loops re-solve nearly the same problem), then one at a time.
 struct Multigrid {
   int nlev = 0, v1 = 2, v2 = 2, v3 = 2;
   std::vector<int> lnx, lny, lP;
   std::vector<double> ldx, ldy;
   std::vector<double*> u, f, r;  // level 0 u/f may alias caller buffers
-  double* part = nullptr;
-  double* d_rms = nullptr;
-  static constexpr int kParts = 512;
+  // fused multi-sweep smoother (mg_smooth_fused_kernel): second u buffer of the levels that
+  // use it; flip[l] = 1 while level l's current iterate lives in alt[l].  Each such level is
+  // smoothed twice per cycle (descent, ascent), so a whole cycle restores flip = 0.
+  std::vector<double*> alt;
+  std::vector<char> fused_lvl, flip;
+  double* part = nullptr;        // block partials of the level-0 residual norm
+  int nparts = 0;
+  int* ctl = nullptr;            // device: [0] converged, [1] norms recorded, [2] spare
+  double* hist = nullptr;        // device residual-norm history
+  int hist_cap = 0;
+  int kc = 0;                    // first level held in LDS by mg_coarse_kernel (nlev: none)
+  MgCoarseArgs ca;
+  size_t coarse_lds = 0;
+  bool use_graph = true;
+  hipGraphExec_t gexec = nullptr;
+  double *g_u0 = nullptr, *g_f0 = nullptr;
+  double g_tol = -1.0;
+  int last_count = 1;
   hipStream_t st = nullptr;
 
   void init(int nx, int ny, double dx, double dy, int n_level, int v1_, int v2_, int v3_,
@@ -303,75 +576,222 @@ struct Multigrid {
       r.push_back(dalloc<double>(n));
       CFDJ_HIP(hipMemset(r[l], 0, n * sizeof(double)));
       if (l) CFDJ_HIP(hipMemset(f[l], 0, n * sizeof(double)));
+      if (l) CFDJ_HIP(hipMemset(u[l], 0, n * sizeof(double)));
     }
-    part = dalloc<double>(kParts);
-    d_rms = dalloc<double>(1);
+    const dim3 g0 = interior_grid(lnx[0], lny[0]);
+    nparts = (int)(g0.x * g0.y);
+    part = dalloc<double>(nparts);
+    ctl = dalloc<int>(4);
+    CFDJ_HIP(hipMemset(ctl, 0, 4 * sizeof(int)));
+    const char* ge = std::getenv("CFDJ_MG_GRAPH");
+    use_graph = !(ge && ge[0] == '0');
+    plan_coarse();
+    // levels smoothed by the fused kernel: both of a level's smoothing calls must use it
+    // (1..3 sweeps each), the level must not be the coarsest (smoothed once per cycle)
+    alt.assign(nlev, nullptr);
+    fused_lvl.assign(nlev, 0);
+    flip.assign(nlev, 0);
+    const char* fe = std::getenv("CFDJ_MG_FUSED_SMOOTH");
+    const bool want = !(fe && fe[0] == '0');
+    auto ok = [](int v) { return v >= 1 && v <= 3; };
+    for (int l = 0; l < nlev && want; ++l) {
+      const bool twice = l < nlev - 1 && (l < kc);
+      if (twice && lnx[l] >= 128 && lny[l] >= 128 && ok(v1) && ok(v3)) {
+        fused_lvl[l] = 1;
+        alt[l] = dalloc<double>((size_t)lP[l] * (lny[l] + 1));
+        CFDJ_HIP(hipMemset(alt[l], 0, (size_t)lP[l] * (lny[l] + 1) * sizeof(double)));
+      }
+    }
   }
+  double* ucur(int l) const { return flip[l] ? alt[l] : u[l]; }
+
+  // Levels kc.. live in LDS when they all fit (every grid <= 64 cells a side).
+  void plan_coarse() {
+    kc = nlev;
+    const char* ce = std::getenv("CFDJ_MG_COARSE");
+    if (ce && ce[0] == '0') return;
+    int first = nlev;
+    for (int l = 1; l < nlev; ++l)
+      if (lnx[l] <= kMgCoarseCells && lny[l] <= kMgCoarseCells) {
+        first = l;
+        break;
+      }
+    if (first >= nlev || nlev - first > kMgCoarseMaxLevels) return;
+    size_t off = 0;
+    ca = MgCoarseArgs();
+    ca.n = nlev - first;
+    for (int c = 0; c < ca.n; ++c) {
+      const int l = first + c;
+      ca.lnx[c] = lnx[l];
+      ca.lny[c] = lny[l];
+      ca.lP[c] = lP[l];
+      ca.dx2[c] = ldx[l] * ldx[l];
+      ca.dy2[c] = ldy[l] * ldy[l];
+      ca.dd[c] = -2.0 / ca.dx2[c] - 2.0 / ca.dy2[c];
+      ca.sweeps_down[c] = l < nlev - 1 ? v1 : v2;
+      const size_t n = (size_t)lP[l] * (lny[l] + 1);
+      ca.off_u[c] = (int)off;
+      off += n;
+      ca.off_f[c] = (int)off;
+      off += n;
+    }
+    ca.off_r = (int)off;
+    off += (size_t)lP[first] * (lny[first] + 1);
+    if (off * sizeof(double) > 150 * 1024) return;
+    coarse_lds = off * sizeof(double);
+    ca.v3 = v3;
+    ca.r_in = r[first - 1];
+    ca.nxf = lnx[first - 1];
+    ca.nyf = lny[first - 1];
+    ca.Pf = lP[first - 1];
+    ca.u_out = u[first];
+    ca.ctl = ctl;
+    CFDJ_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mg_coarse_kernel),
+                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)coarse_lds));
+    kc = first;
+  }
+
   void destroy() {
+    if (gexec) (void)hipGraphExecDestroy(gexec);
+    gexec = nullptr;
     for (int l = 1; l < nlev; ++l) {
       dfree(u[l]);
       dfree(f[l]);
     }
     for (auto& p : r) dfree(p);
+    for (auto& p : alt) dfree(p);
     dfree(part);
-    dfree(d_rms);
+    dfree(ctl);
+    dfree(hist);
   }
   void smooth(int l, int sweeps) {
     const double dx2 = ldx[l] * ldx[l], dy2 = ldy[l] * ldy[l];
     const double dd = -2.0 / dx2 - 2.0 / dy2;
+    if (fused_lvl[l] && sweeps >= 1 && sweeps <= 3) {
+      const dim3 g((lnx[l] + 1 + kFsTX - 1) / kFsTX, (lny[l] + 1 + kFsTY - 1) / kFsTY);
+      const double* in = ucur(l);
+      flip[l] ^= 1;
+      double* out = ucur(l);
+      switch (sweeps) {
+        case 1: hipLaunchKernelGGL(mg_smooth_fused_kernel<1>, g, dim3(256), 0, st, f[l], in, out, lnx[l], lny[l], lP[l], dx2, dy2, dd, ctl); break;
+        case 2: hipLaunchKernelGGL(mg_smooth_fused_kernel<2>, g, dim3(256), 0, st, f[l], in, out, lnx[l], lny[l], lP[l], dx2, dy2, dd, ctl); break;
+        default: hipLaunchKernelGGL(mg_smooth_fused_kernel<3>, g, dim3(256), 0, st, f[l], in, out, lnx[l], lny[l], lP[l], dx2, dy2, dd, ctl); break;
+      }
+      return;
+    }
     dim3 g((lnx[l] / 2 + kBX - 1) / kBX, (lny[l] - 1 + kBY - 1) / kBY);
     for (int s = 0; s < sweeps; ++s)
       for (int parity = 0; parity < 2; ++parity)
-        hipLaunchKernelGGL(rbgs_kernel, g, dim3(kBX, kBY), 0, st, f[l], u[l], lnx[l], lny[l],
-                           lP[l], dx2, dy2, dd, parity);
+        hipLaunchKernelGGL(mg_rbgs_kernel, g, dim3(kBX, kBY), 0, st, f[l], ucur(l), lnx[l],
+                           lny[l], lP[l], dx2, dy2, dd, parity, ctl);
+  }
+  void residual(int l, bool with_norm) {
+    hipLaunchKernelGGL(mg_residual_kernel, interior_grid(lnx[l], lny[l]), dim3(kBX, kBY), 0, st,
+                       f[l], ucur(l), r[l], lnx[l], lny[l], lP[l], ldx[l] * ldx[l],
+                       ldy[l] * ldy[l], with_norm ? part : nullptr, ctl);
+  }
+  void norm0(double tol, bool first) {  // Common.jl:229-232 of level 0's residual
+    hipLaunchKernelGGL(mg_norm_kernel, dim3(1), dim3(256), 0, st, part, nparts,
+                       (double)(lnx[0] - 1) * (lny[0] - 1), hist, hist_cap, ctl, tol,
+                       first ? 1 : 0);
+  }
+
+  // One iteration of the mg_N.jl:53-106 loop body.
+  void cycle(double tol) {
+    smooth(0, v1);
+    residual(0, true);
+    norm0(tol, false);
+    for (int k = 1; k < nlev && k < kc; ++k) {
+      if (k > 1) residual(k - 1, false);
+      hipLaunchKernelGGL(mg_restrict_kernel,
+                         dim3((lnx[k] + 1 + kBX - 1) / kBX, (lny[k] + 1 + kBY - 1) / kBY),
+                         dim3(kBX, kBY), 0, st, r[k - 1], f[k], ucur(k), lnx[k - 1], lny[k - 1],
+                         lP[k - 1], lnx[k], lny[k], lP[k], ctl);
+      smooth(k, k < nlev - 1 ? v1 : v2);
+    }
+    if (kc < nlev) {
+      if (kc > 1) residual(kc - 1, false);
+      hipLaunchKernelGGL(mg_coarse_kernel, dim3(1), dim3(1024), coarse_lds, st, ca);
+    }
+    for (int k = (kc < nlev ? kc : nlev - 1); k >= 1; --k) {
+      hipLaunchKernelGGL(mg_prolong_add_kernel, interior_grid(lnx[k - 1], lny[k - 1]),
+                         dim3(kBX, kBY), 0, st, ucur(k), ucur(k - 1), lnx[k - 1], lny[k - 1],
+                         lP[k - 1], lP[k], ctl);
+      smooth(k - 1, v3);
+    }
     CFDJ_HIP(hipGetLastError());
+    for (int l = 0; l < nlev; ++l)
+      if (flip[l]) throw Error{CFDJ_ERR_STATE, "multigrid: smoothing buffers out of phase"};
   }
-  void residual(int l) {
-    hipLaunchKernelGGL(residual_kernel, interior_grid(lnx[l], lny[l]), dim3(kBX, kBY), 0, st,
-                       f[l], u[l], r[l], lnx[l], lny[l], lP[l], ldx[l] * ldx[l],
-                       ldy[l] * ldy[l]);
-    CFDJ_HIP(hipGetLastError());
+
+  void launch_cycles(int n, double tol) {
+    if (!use_graph) {
+      for (int i = 0; i < n; ++i) cycle(tol);
+      return;
+    }
+    if (!gexec || g_u0 != u[0] || g_f0 != f[0] || g_tol != tol) {
+      if (gexec) (void)hipGraphExecDestroy(gexec);
+      gexec = nullptr;
+      hipGraph_t g = nullptr;
+      CFDJ_HIP(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+      try {
+        cycle(tol);
+      } catch (...) {
+        (void)hipStreamEndCapture(st, &g);
+        if (g) (void)hipGraphDestroy(g);
+        throw;
+      }
+      CFDJ_HIP(hipStreamEndCapture(st, &g));
+      const hipError_t e = hipGraphInstantiate(&gexec, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      CFDJ_HIP(e);
+      g_u0 = u[0];
+      g_f0 = f[0];
+      g_tol = tol;
+    }
+    for (int i = 0; i < n; ++i) CFDJ_HIP(hipGraphLaunch(gexec, st));
   }
-  double l2norm0() {  // Common.jl:229-232 on level 0's residual (host sync)
-    launch_rms(r[0], nullptr, 1, lnx[0] - 1, 1, lny[0] - 1, lP[0],
-               (double)(lnx[0] - 1) * (lny[0] - 1), part, kParts, d_rms, st);
-    double h = 0.0;
-    CFDJ_HIP(hipMemcpyAsync(&h, d_rms, sizeof(double), hipMemcpyDeviceToHost, st));
-    CFDJ_HIP(hipStreamSynchronize(st));
-    return h;
-  }
+
   // Solve on level-0 buffers u0 (in/out, boundary = Dirichlet data) and f0 (pitch nx+2).
-  int solve(double* u0, double* f0, double tol, int max_iter, std::vector<double>* hist) {
+  int solve(double* u0, double* f0, double tol, int max_iter, std::vector<double>* hist_out) {
     u[0] = u0;
     f[0] = f0;
-    residual(0);
-    const double init_rms = l2norm0();
-    double rms = init_rms;
-    if (hist) hist->push_back(rms);
-    int it = 0;
-    while (it < max_iter) {
-      ++it;
-      smooth(0, v1);
-      residual(0);
-      rms = l2norm0();
-      if (hist) hist->push_back(rms);
-      if (!(rms / init_rms > tol)) break;  // also stops on init_rms == 0
-      for (int k = 1; k < nlev; ++k) {
-        if (k > 1) residual(k - 1);
-        hipLaunchKernelGGL(restriction_kernel,
-                           dim3((lnx[k] + 1 + kBX - 1) / kBX, (lny[k] + 1 + kBY - 1) / kBY),
-                           dim3(kBX, kBY), 0, st, r[k - 1], f[k], lnx[k - 1], lny[k - 1],
-                           lP[k - 1], lnx[k], lny[k], lP[k]);
-        CFDJ_HIP(hipMemsetAsync(u[k], 0, (size_t)lP[k] * (lny[k] + 1) * sizeof(double), st));
-        smooth(k, k < nlev - 1 ? v1 : v2);
-      }
-      for (int k = nlev - 1; k >= 1; --k) {
-        hipLaunchKernelGGL(prolong_add_kernel, interior_grid(lnx[k - 1], lny[k - 1]),
-                           dim3(kBX, kBY), 0, st, u[k], u[k - 1], lnx[k - 1], lny[k - 1],
-                           lP[k - 1], lP[k]);
-        smooth(k - 1, v3);
-      }
-      CFDJ_HIP(hipGetLastError());
+    const int want = (hist_out ? max_iter : 0) + 2;
+    if (want > hist_cap) {  // the history is kept only when the caller asks for it
+      dfree(hist);
+      hist = dalloc<double>(want);
+      hist_cap = want;
+      if (gexec) (void)hipGraphExecDestroy(gexec);  // the norm node holds the old pointer
+      gexec = nullptr;
+    }
+    CFDJ_HIP(hipMemsetAsync(ctl, 0, 4 * sizeof(int), st));
+    residual(0, true);
+    norm0(tol, true);
+    int host_ctl[4] = {0, 0, 0, 0};
+    int launched = 0;
+    int batch = last_count < 1 ? 1 : last_count;
+    while (launched < max_iter) {
+      if (batch > max_iter - launched) batch = max_iter - launched;
+      launch_cycles(batch, tol);
+      launched += batch;
+      CFDJ_HIP(hipMemcpyAsync(host_ctl, ctl, sizeof(host_ctl), hipMemcpyDeviceToHost, st));
+      CFDJ_HIP(hipStreamSynchronize(st));
+      if (host_ctl[0]) break;
+      batch = 1;
+    }
+    const int it = max_iter > 0 ? host_ctl[1] - 1 : 0;
+    if (max_iter == 0) CFDJ_HIP(hipStreamSynchronize(st));
+    last_count = it;
+    // the converged iterate is the output of the cycle's first smoothing call (mg_N.jl:56,
+    // 70): with the fused smoother on level 0 it sits in the second buffer
+    if (host_ctl[0] && fused_lvl[0])
+      CFDJ_HIP(hipMemcpyAsync(u0, alt[0], (size_t)lP[0] * (lny[0] + 1) * sizeof(double),
+                              hipMemcpyDeviceToDevice, st));
+    if (hist_out) {
+      hist_out->resize((size_t)it + 1);
+      CFDJ_HIP(hipMemcpyAsync(hist_out->data(), hist, ((size_t)it + 1) * sizeof(double),
+                              hipMemcpyDeviceToHost, st));
+      CFDJ_HIP(hipStreamSynchronize(st));
     }
     return it;
   }

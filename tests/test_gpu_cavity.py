@@ -150,3 +150,31 @@ def test_gpu_cavity_main_writes_reference_files(lib, tmp_path):
     assert np.array_equal(read_field(tmp_path / "field_final.txt", n, n, 3), sn)
     xy = np.loadtxt(tmp_path / "field_final.txt")[:, :2]
     assert xy[1, 0] == 1.0 / n and xy[n + 1, 1] == 1.0 / n
+
+
+@pytest.mark.parametrize("n,levels,sweeps", [(512, 9, (2, 2, 2)), (512, 9, (2, 1, 3)),
+                                             (256, 4, (1, 2, 1)), (1024, 10, (3, 2, 2))])
+def test_gpu_mg_fused_kernels_are_bit_identical(lib, monkeypatch, n, levels, sweeps):
+    """The V-cycle's fused kernels (several red-black sweeps per pass over a level in LDS
+    tiles; all coarse levels in one workgroup; cycles replayed from a HIP graph) reorder no
+    arithmetic: iterates, iteration count and residual history equal the one-launch-per-
+    half-sweep, level-by-level, eagerly launched V-cycle bit for bit."""
+    from cfd_julia_amd import mg
+
+    v1, v2, v3 = sweeps
+    out = {}
+    for name, env in (("fused", {}),
+                      ("plain", {"CFDJ_MG_FUSED_SMOOTH": "0", "CFDJ_MG_COARSE": "0",
+                                 "CFDJ_MG_GRAPH": "0"})):
+        for k in ("CFDJ_MG_FUSED_SMOOTH", "CFDJ_MG_COARSE", "CFDJ_MG_GRAPH"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        f, ue, un, dx, dy = mg.mms(n, ipr=2)
+        r = np.zeros((n + 1, n + 1), order="F")
+        it, hist = mg.mg_N(dx, dy, n, n, r, f, un, v1, v2, v3, 100000, 1e-9, n_level=levels)
+        out[name] = (it, hist, un, r)
+    assert out["fused"][0] == out["plain"][0] and out["fused"][0] > 2
+    assert np.array_equal(out["fused"][1], out["plain"][1])
+    assert np.array_equal(out["fused"][2], out["plain"][2])
+    assert np.array_equal(out["fused"][3], out["plain"][3])
