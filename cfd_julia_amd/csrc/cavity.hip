@@ -219,65 +219,118 @@ __global__ __launch_bounds__(kBX* kBY) void mg_rbgs_kernel(const double* __restr
 }
 
 // S full red-black sweeps (2S half sweeps) of the same update in ONE pass over the level:
-// a workgroup loads its 64 x 32 tile of u and f plus a halo of 2S nodes into LDS, runs the
+// a workgroup loads its (128 - 4S) x 24 tile of u and f plus a halo of 2S nodes into LDS, runs the
 // half sweeps there (each one valid on a region one node smaller all round: an update needs
 // its four neighbours' values of the previous half sweep), and writes the tile to `uout`.
 // Every point of the tile sees exactly the neighbour values the separate half-sweep
 // launches would give it, so the result is bit-identical to them; HBM traffic per call is
 // f + u in + u out (24 B per node) instead of 2S x (f + u + u).  Out of place: neighbouring
 // tiles read each other's old values (the caller ping-pongs the two buffers).
-constexpr int kFsTX = 64, kFsTY = 32;
-template <int S>
+//
+// RCP: dx^2, dy^2 and the diagonal -2/dx^2 - 2/dy^2 are exact powers of two (any 2^k-cell
+// unit box), so the three divisions of the update are multiplications by the exact
+// reciprocals passed in their place -- the same bits, a third of the instructions (with the
+// data in LDS the kernel is bound by that arithmetic, not by memory).
+constexpr int kFsW = 128, kFsTY = 24;  // LDS row of 128 nodes: tile = (128 - 4S) x 24 nodes
+template <bool RCP>
+__device__ __forceinline__ double mg_div(double x, double d) {
+  return RCP ? x * d : x / d;
+}
+//
+// ucor != nullptr: the coarse-grid correction of the ascent (Common.jl:50-76 prolongation +
+// mg_N.jl:99-101) is added to the interior nodes while the tile is loaded, instead of a
+// separate pass over u before the smoothing.
+//
+// Thread layout: 64 lanes along x (one lane per pair of nodes of a 128-node LDS row: the
+// lane's node of the half sweep's colour), 4 wavefronts taking every fourth row.
+template <int S, bool RCP>
 __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __restrict__ f,
                                                               const double* __restrict__ uin,
                                                               double* __restrict__ uout, int nx,
                                                               int ny, int P, double dx2,
                                                               double dy2, double dd,
+                                                              const double* __restrict__ ucor,
+                                                              int Pc,
                                                               const int* __restrict__ ctl) {
   if (mg_done(ctl)) return;
-  constexpr int H = 2 * S, W = kFsTX + 2 * H, HT = kFsTY + 2 * H;
+  constexpr int H = 2 * S, W = kFsW, TX = W - 2 * H, HT = kFsTY + 2 * H;
   __shared__ double su[HT * W];
   __shared__ double sf[HT * W];
-  const int x0 = blockIdx.x * kFsTX - H, y0 = blockIdx.y * kFsTY - H;  // node of local (0, 0)
-  for (int e = threadIdx.x; e < W * HT; e += 256) {
-    const int lj = e / W, li = e % W;
-    const int gi = x0 + li, gj = y0 + lj;
-    double uv = 0.0, fv = 0.0;
-    if (gi >= 0 && gi <= nx && gj >= 0 && gj <= ny) {
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int x0 = blockIdx.x * TX - H, y0 = blockIdx.y * kFsTY - H;  // node of local (0, 0)
+  // load: one 16-B access per lane covers a whole 128-node row (x0 and the pitch are even,
+  // so the pair (gi, gi + 1) is aligned; gi + 1 = nx + 1 is the arrays' padding column);
+  // all of a wavefront's rows are requested before the first one is used
+  constexpr int ROWS = HT / 4;
+  static_assert(HT % 4 == 0, "rows per wavefront");
+  const int gi = x0 + 2 * tx;
+  const bool xin = gi >= 0 && gi <= nx;
+  double2 ru[ROWS], rf[ROWS];
+#pragma unroll
+  for (int k = 0; k < ROWS; ++k) {
+    const int gj = y0 + ty + 4 * k;
+    ru[k] = make_double2(0.0, 0.0);
+    rf[k] = make_double2(0.0, 0.0);
+    if (xin && gj >= 0 && gj <= ny) {
       const size_t c = (size_t)gj * P + gi;
-      uv = uin[c];
-      fv = f[c];
+      ru[k] = *reinterpret_cast<const double2*>(uin + c);
+      rf[k] = *reinterpret_cast<const double2*>(f + c);
     }
-    su[e] = uv;
-    sf[e] = fv;
+  }
+#pragma unroll
+  for (int k = 0; k < ROWS; ++k) {
+    const int lj = ty + 4 * k, gj = y0 + lj;
+    if (ucor != nullptr && gj >= 1 && gj < ny) {
+      const size_t qr = (size_t)(gj >> 1) * Pc;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int g = gi + e;
+        if (g >= 1 && g < nx) {
+          const size_t q = qr + (g >> 1);
+          double p;
+          if (!(g & 1) && !(gj & 1)) p = ucor[q];
+          else if (!(g & 1)) p = 0.5 * (ucor[q] + ucor[q + Pc]);
+          else if (!(gj & 1)) p = 0.5 * (ucor[q] + ucor[q + 1]);
+          else p = 0.25 * (ucor[q] + ucor[q + Pc] + ucor[q + 1] + ucor[q + Pc + 1]);
+          if (e == 0) ru[k].x += p;
+          else ru[k].y += p;
+        }
+      }
+    }
+    if (gi + 1 > nx) {  // the padding column is not a node
+      ru[k].y = 0.0;
+      rf[k].y = 0.0;
+    }
+    *reinterpret_cast<double2*>(su + lj * W + 2 * tx) = ru[k];
+    *reinterpret_cast<double2*>(sf + lj * W + 2 * tx) = rf[k];
   }
   __syncthreads();
 #pragma unroll 1
   for (int h = 1; h <= 2 * S; ++h) {
     const int parity = (h - 1) & 1;
-    const int wdt = W - 2 * h, hgt = HT - 2 * h;  // local region [h, W-1-h] x [h, HT-1-h]
-    const int hw = (wdt + 1) / 2;
-    for (int e = threadIdx.x; e < hw * hgt; e += 256) {
-      const int lj = h + e / hw;
+    // valid region of this half sweep: local [h, W-1-h] x [h, HT-1-h]
+    for (int lj = h + ty; lj <= HT - 1 - h; lj += 4) {
       const int gj = y0 + lj;
-      // first local column >= h whose node has (gi + gj) % 2 == parity
-      const int li = h + 2 * (e % hw) + ((x0 + h + gj + parity) & 1);
-      const int gi = x0 + li;
-      if (li <= W - 1 - h && gi >= 1 && gi < nx && gj >= 1 && gj < ny) {
+      const int li = 2 * tx + ((x0 + gj + parity) & 1);  // (node x + gj) % 2 == parity
+      const int gx = x0 + li;
+      if (li >= h && li <= W - 1 - h && gx >= 1 && gx < nx && gj >= 1 && gj < ny) {
         const int c = lj * W + li;
         const double uc = su[c];
-        const double rt = sf[c] - ((su[c + 1] - 2.0 * uc + su[c - 1]) / dx2 +
-                                   (su[c + W] - 2.0 * uc + su[c - W]) / dy2);
-        su[c] = uc + rt / dd;
+        const double rt = sf[c] - (mg_div<RCP>(su[c + 1] - 2.0 * uc + su[c - 1], dx2) +
+                                   mg_div<RCP>(su[c + W] - 2.0 * uc + su[c - W], dy2));
+        su[c] = uc + mg_div<RCP>(rt, dd);
       }
     }
     __syncthreads();
   }
-  for (int e = threadIdx.x; e < kFsTX * kFsTY; e += 256) {
-    const int lj = H + e / kFsTX, li = H + e % kFsTX;
-    const int gi = x0 + li, gj = y0 + lj;
-    if (gi <= nx && gj <= ny) uout[(size_t)gj * P + gi] = su[lj * W + li];
-  }
+  if (2 * tx >= H && 2 * tx < H + TX && gi <= nx)
+    for (int lj = H + ty; lj < H + kFsTY; lj += 4) {
+      const int gj = y0 + lj;
+      if (gj > ny) break;
+      const double2 v = *reinterpret_cast<const double2*>(su + lj * W + 2 * tx);
+      if (gi + 1 <= nx) *reinterpret_cast<double2*>(uout + (size_t)gj * P + gi) = v;
+      else uout[(size_t)gj * P + gi] = v.x;
+    }
 }
 
 // Common.jl:239-246 residual; with part != nullptr also this block's sum of r^2 (fixed
@@ -313,18 +366,18 @@ __global__ __launch_bounds__(kBX* kBY) void mg_residual_kernel(const double* __r
 
 // rms = sqrt(sum of the block partials / denom) -> hist[ctl[1]++]; first = 1: the initial
 // residual (mg_N.jl:22, no test); else the convergence test of mg_N.jl:70 against hist[0].
-__global__ __launch_bounds__(256) void mg_norm_kernel(const double* __restrict__ part,
-                                                      int nparts, double denom,
-                                                      double* __restrict__ hist, int hist_cap,
-                                                      int* __restrict__ ctl, double tol,
-                                                      int first) {
+__global__ __launch_bounds__(1024) void mg_norm_kernel(const double* __restrict__ part,
+                                                       int nparts, double denom,
+                                                       double* __restrict__ hist, int hist_cap,
+                                                       int* __restrict__ ctl, double tol,
+                                                       int first) {
   if (mg_done(ctl)) return;
-  __shared__ double red[256];
+  __shared__ double red[1024];
   double acc = 0.0;
   for (int i = threadIdx.x; i < nparts; i += blockDim.x) acc += part[i];
   red[threadIdx.x] = acc;
   __syncthreads();
-  for (int off = 128; off > 0; off >>= 1) {
+  for (int off = 512; off > 0; off >>= 1) {
     if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
     __syncthreads();
   }
@@ -664,19 +717,39 @@ struct Multigrid {
     dfree(ctl);
     dfree(hist);
   }
-  void smooth(int l, int sweeps) {
+  // `sweeps` red-black sweeps on level l; cor >= 0: first add the prolongation of level
+  // cor's iterate (the ascent's correction step).
+  void smooth(int l, int sweeps, int cor = -1) {
     const double dx2 = ldx[l] * ldx[l], dy2 = ldy[l] * ldy[l];
     const double dd = -2.0 / dx2 - 2.0 / dy2;
-    if (fused_lvl[l] && sweeps >= 1 && sweeps <= 3) {
-      const dim3 g((lnx[l] + 1 + kFsTX - 1) / kFsTX, (lny[l] + 1 + kFsTY - 1) / kFsTY);
+    const bool fuse = fused_lvl[l] && sweeps >= 1 && sweeps <= 3;
+    if (cor >= 0 && !fuse)
+      hipLaunchKernelGGL(mg_prolong_add_kernel, interior_grid(lnx[l], lny[l]), dim3(kBX, kBY), 0,
+                         st, ucur(cor), ucur(l), lnx[l], lny[l], lP[l], lP[cor], ctl);
+    if (fuse) {
+      const double* ucor = cor >= 0 ? ucur(cor) : nullptr;
+      const int Pc = cor >= 0 ? lP[cor] : 0;
+      const int tx = kFsW - 4 * sweeps;  // tile width of mg_smooth_fused_kernel<sweeps>
+      const dim3 g((lnx[l] + 1 + tx - 1) / tx, (lny[l] + 1 + kFsTY - 1) / kFsTY);
       const double* in = ucur(l);
       flip[l] ^= 1;
       double* out = ucur(l);
+      auto pow2 = [](double d) {
+        int e = 0;
+        const double m = std::frexp(std::fabs(d), &e);
+        return m == 0.5 && e > -500 && e < 500;
+      };
+      const bool rcp = pow2(dx2) && pow2(dy2) && pow2(dd);
+      const double a = rcp ? 1.0 / dx2 : dx2, b = rcp ? 1.0 / dy2 : dy2, c = rcp ? 1.0 / dd : dd;
+#define CFDJ_FS(S, R)                                                                           \
+  hipLaunchKernelGGL((mg_smooth_fused_kernel<S, R>), g, dim3(256), 0, st, f[l], in, out, lnx[l], \
+                     lny[l], lP[l], a, b, c, ucor, Pc, ctl)
       switch (sweeps) {
-        case 1: hipLaunchKernelGGL(mg_smooth_fused_kernel<1>, g, dim3(256), 0, st, f[l], in, out, lnx[l], lny[l], lP[l], dx2, dy2, dd, ctl); break;
-        case 2: hipLaunchKernelGGL(mg_smooth_fused_kernel<2>, g, dim3(256), 0, st, f[l], in, out, lnx[l], lny[l], lP[l], dx2, dy2, dd, ctl); break;
-        default: hipLaunchKernelGGL(mg_smooth_fused_kernel<3>, g, dim3(256), 0, st, f[l], in, out, lnx[l], lny[l], lP[l], dx2, dy2, dd, ctl); break;
+        case 1: if (rcp) CFDJ_FS(1, true); else CFDJ_FS(1, false); break;
+        case 2: if (rcp) CFDJ_FS(2, true); else CFDJ_FS(2, false); break;
+        default: if (rcp) CFDJ_FS(3, true); else CFDJ_FS(3, false); break;
       }
+#undef CFDJ_FS
       return;
     }
     dim3 g((lnx[l] / 2 + kBX - 1) / kBX, (lny[l] - 1 + kBY - 1) / kBY);
@@ -691,7 +764,7 @@ struct Multigrid {
                        ldy[l] * ldy[l], with_norm ? part : nullptr, ctl);
   }
   void norm0(double tol, bool first) {  // Common.jl:229-232 of level 0's residual
-    hipLaunchKernelGGL(mg_norm_kernel, dim3(1), dim3(256), 0, st, part, nparts,
+    hipLaunchKernelGGL(mg_norm_kernel, dim3(1), dim3(1024), 0, st, part, nparts,
                        (double)(lnx[0] - 1) * (lny[0] - 1), hist, hist_cap, ctl, tol,
                        first ? 1 : 0);
   }
@@ -713,12 +786,7 @@ struct Multigrid {
       if (kc > 1) residual(kc - 1, false);
       hipLaunchKernelGGL(mg_coarse_kernel, dim3(1), dim3(1024), coarse_lds, st, ca);
     }
-    for (int k = (kc < nlev ? kc : nlev - 1); k >= 1; --k) {
-      hipLaunchKernelGGL(mg_prolong_add_kernel, interior_grid(lnx[k - 1], lny[k - 1]),
-                         dim3(kBX, kBY), 0, st, ucur(k), ucur(k - 1), lnx[k - 1], lny[k - 1],
-                         lP[k - 1], lP[k], ctl);
-      smooth(k - 1, v3);
-    }
+    for (int k = (kc < nlev ? kc : nlev - 1); k >= 1; --k) smooth(k - 1, v3, k);
     CFDJ_HIP(hipGetLastError());
     for (int l = 0; l < nlev; ++l)
       if (flip[l]) throw Error{CFDJ_ERR_STATE, "multigrid: smoothing buffers out of phase"};

@@ -153,7 +153,8 @@ def test_gpu_cavity_main_writes_reference_files(lib, tmp_path):
 
 
 @pytest.mark.parametrize("n,levels,sweeps", [(512, 9, (2, 2, 2)), (512, 9, (2, 1, 3)),
-                                             (256, 4, (1, 2, 1)), (1024, 10, (3, 2, 2))])
+                                             (256, 4, (1, 2, 1)), (1024, 10, (3, 2, 2)),
+                                             (384, 3, (2, 2, 2))])
 def test_gpu_mg_fused_kernels_are_bit_identical(lib, monkeypatch, n, levels, sweeps):
     """The V-cycle's fused kernels (several red-black sweeps per pass over a level in LDS
     tiles; all coarse levels in one workgroup; cycles replayed from a HIP graph) reorder no
