@@ -32,15 +32,21 @@ namespace {
 // ---------------------------------------------------------------------------------------
 // Pass 1: rows, real -> packed half spectrum, column-major output H[m][y].
 // ---------------------------------------------------------------------------------------
-template <int L>
+template <int L, bool FWD = true>
 struct RowCfg {
   static constexpr int T = Plan<L>::T;
   // rows per work item: >= 4 (64-B column segments) where the LDS holds them, fewer for
   // the long rows of the multi-GPU grids (L = 4096: 2, L = 8192: 1 -- 136 KB per row)
-#ifndef CFDJ_ROWS_XR_MIN
-#define CFDJ_ROWS_XR_MIN 4
+  // (separately for the forward and the inverse pass: the segment size is an access
+  // pattern of each pass, not a property of the spectrum layout)
+#ifndef CFDJ_ROWS_FWD_XR_MIN
+#define CFDJ_ROWS_FWD_XR_MIN 4
 #endif
-  static constexpr int XR_WANT = (256 / T) > CFDJ_ROWS_XR_MIN ? (256 / T) : CFDJ_ROWS_XR_MIN;
+#ifndef CFDJ_ROWS_INV_XR_MIN
+#define CFDJ_ROWS_INV_XR_MIN 4
+#endif
+  static constexpr int XR_MIN = FWD ? CFDJ_ROWS_FWD_XR_MIN : CFDJ_ROWS_INV_XR_MIN;
+  static constexpr int XR_WANT = (256 / T) > XR_MIN ? (256 / T) : XR_MIN;
   static constexpr int XR_FIT = (140 * 1024) / (Plan<L>::ROWSTRIDE * 16);
   static constexpr int XR = XR_WANT < XR_FIT ? XR_WANT : XR_FIT;
   static_assert(XR >= 1, "row does not fit the LDS");
@@ -51,9 +57,9 @@ struct RowCfg {
 // Element pair p of a work item: row qq, columns m and L-m (m = p in [0, L/2)).  Lanes take
 // 16 consecutive m of one row, so both LDS accesses are contiguous per row and both global
 // accesses cover whole XR*16-B column segments.
-template <int L>
+template <int L, bool FWD>
 __device__ __forceinline__ void pair_index(int e, int& qq, int& m) {
-  using C = RowCfg<L>;
+  using C = RowCfg<L, FWD>;
   qq = (e >> 4) % C::XR;
   m = ((e >> 4) / C::XR) * 16 + (e & 15);
 }
@@ -98,7 +104,7 @@ __device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, 
                                               int next_y0, int q, int tid,
                                               const TwLds<L>& twL, const TwLds<2 * L>& twN) {
   using P = Plan<L>;
-  using C = RowCfg<L>;
+  using C = RowCfg<L, true>;
   stage_regs<L, 0, -1>(nxt, tid, twL);
   lds_write<L, 0>(buf, nxt, tid);
   if (next_y0 >= 0) load_row_z<L>(nxt, f, next_y0 + q, tid);
@@ -114,7 +120,7 @@ __device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, 
 #pragma unroll
   for (int i = 0; i < C::PAIRS; ++i) {
     int qq, m;
-    pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+    pair_index<L, true>(threadIdx.x + i * C::THREADS, qq, m);
     const bool z0 = i == 0 && m == 0;
     const int mp = z0 ? L / 2 : L - m;
     const double2* bq = lds + qq * P::ROWSTRIDE;
@@ -141,11 +147,11 @@ __device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, 
 }
 
 template <int L, bool TILE>
-__global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_fwd_kernel(
+__global__ __launch_bounds__((RowCfg<L, true>::THREADS)) void rows_fwd_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
   using P = Plan<L>;
-  using C = RowCfg<L>;
+  using C = RowCfg<L, true>;
   __shared__ double2 lds[C::XR * P::ROWSTRIDE];
   __shared__ TwLds<L> twL;      // W_L (row FFT stages)
   __shared__ TwLds<2 * L> twN;  // W_N (r2c post-processing)
@@ -311,13 +317,13 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(const double2* __restr
 // Z[L-m] = conj of the same expression with m and L-m swapped.
 template <int L>
 struct InvLoads {
-  double2 xm[RowCfg<L>::PAIRS], xp[RowCfg<L>::PAIRS];
+  double2 xm[RowCfg<L, false>::PAIRS], xp[RowCfg<L, false>::PAIRS];
   double2 xh;  // X[L/2] for the thread that owns m = 0
 };
 template <int L, bool TILE>
 __device__ __forceinline__ void load_inv(InvLoads<L>& ld, const double2* __restrict__ H, int M,
                                          int y0) {
-  using C = RowCfg<L>;
+  using C = RowCfg<L, false>;
   // uniform row offset in the base pointer, 32-bit per-lane offsets (sidx(m, y0 + qq) =
   // sidx(m, qq) + sidx(0, y0) in both layouts)
   const double2* base = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
@@ -329,7 +335,7 @@ __device__ __forceinline__ void load_inv(InvLoads<L>& ld, const double2* __restr
 #pragma unroll
   for (int i = 0; i < C::PAIRS; ++i) {
     int qq, m;
-    pair_index<L>(tx + i * C::THREADS, qq, m);
+    pair_index<L, false>(tx + i * C::THREADS, qq, m);
     ld.xm[i] = base[(unsigned)sidx<TILE>(m, qq, M)];
     ld.xp[i] = base[(unsigned)sidx<TILE>((L - m) & (L - 1), qq, M)];  // m = 0: unused
     // m = 0 occurs in pair 0 only (later pairs start at m >= 16); every lane loads, the
@@ -349,11 +355,11 @@ __device__ __forceinline__ void rows_inv_item(InvLoads<L>& nxt, double2* lds, do
                                               int next_y0, int q, int tid,
                                               const TwLds<L>& twL, const TwLds<2 * L>& twN) {
   using P = Plan<L>;
-  using C = RowCfg<L>;
+  using C = RowCfg<L, false>;
 #pragma unroll
   for (int i = 0; i < C::PAIRS; ++i) {
     int qq, m;
-    pair_index<L>(threadIdx.x + i * C::THREADS, qq, m);
+    pair_index<L, false>(threadIdx.x + i * C::THREADS, qq, m);
     const bool z0 = i == 0 && m == 0;
     double2* bq = lds + qq * P::ROWSTRIDE;
     const double2 Xm = nxt.xm[i];
@@ -388,11 +394,11 @@ __device__ __forceinline__ void rows_inv_item(InvLoads<L>& nxt, double2* lds, do
 }
 
 template <int L, bool TILE>
-__global__ __launch_bounds__(RowCfg<L>::THREADS) void rows_inv_kernel(
+__global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
   using P = Plan<L>;
-  using C = RowCfg<L>;
+  using C = RowCfg<L, false>;
   __shared__ double2 lds[C::XR * P::ROWSTRIDE];
   __shared__ TwLds<L> twL;
   __shared__ TwLds<2 * L> twN;
@@ -425,14 +431,23 @@ static int persistent_grid(int ncu, int per_cu, int items) {
   return nb < items ? nb : items;
 }
 
+template <int L, bool FWD>
+void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st);
+
 template <int L>
 void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  using C = RowCfg<L>;
+  if (pass == 0) launch_rows_dir<L, true>(pass, a, st);
+  else launch_rows_dir<L, false>(pass, a, st);
+}
+
+template <int L, bool FWD>
+void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st) {
+  using C = RowCfg<L, FWD>;
   constexpr int row_lds = C::XR * Plan<L>::ROWSTRIDE * 16 + sizeof(TwLds<L>) +
                           sizeof(TwLds<2 * L>);
   const int per_cu = (160 * 1024) / row_lds;
   const dim3 grid(persistent_grid(a.ncu, per_cu, a.rows / C::XR));
-  if (pass == 0) {
+  if constexpr (FWD) {
     if (a.tile8)
       hipLaunchKernelGGL((rows_fwd_kernel<L, true>), grid, dim3(C::THREADS), 0, st, a.f, a.H,
                          a.rows, a.twL, a.twN);

@@ -3,6 +3,7 @@
 // Build: hipcc --offload-arch=gfx950 -O3 tools/micro/streambench.hip -o tools/micro/streambench
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <vector>
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); return 1; } } while (0)
 
@@ -66,8 +67,9 @@ __global__ __launch_bounds__(256) void march_kernel(const double* __restrict__ a
   }
 }
 
-int main() {
-  const int nx = 4096, ny = 4096;
+int main(int argc, char** argv) {
+  const int nx = argc > 1 ? atoi(argv[1]) : 4096, ny = argc > 2 ? atoi(argv[2]) : nx;
+  printf("arrays of %d x %d doubles (%.0f MB each)\n", nx, ny, (double)nx * ny * 8 / 1e6);
   const size_t n = (size_t)nx * ny, n2 = n / 2;
   double *a, *b, *c, *o;
   CK(hipMalloc(&a, n * 8)); CK(hipMalloc(&b, n * 8)); CK(hipMalloc(&c, n * 8)); CK(hipMalloc(&o, n * 8));
