@@ -940,6 +940,8 @@ struct cfdj_cavity {
     a.twX = twX;
     a.twY = twY;
     a.ncu = ncu;
+    a.sprev = nullptr;
+    a.part = nullptr;
     return a;
   }
 
@@ -994,7 +996,8 @@ struct cfdj_cavity {
     return k;
   }
 
-  void stage(int st_, const double* w, double* out, double dt) {
+  void stage(int st_, const double* w, double* out, double dt) { stage(st_, w, out, dt, sn); }
+  void stage(int st_, const double* w, double* out, double dt, const double* sn) {
     const CavCoef k = coef(dt);
     const dim3 g = interior_grid(nx, ny), b(kBX, kBY);
     switch (st_) {
@@ -1006,7 +1009,8 @@ struct cfdj_cavity {
     CFDJ_HIP(hipGetLastError());
   }
 
-  void bc2(double* w) {
+  void bc2(double* w) { bc2(w, sn); }
+  void bc2(double* w, const double* sn) {
     hipLaunchKernelGGL(bc2_kernel, dim3((nx + ny + 255) / 256), dim3(256), 0, stream, w, sn,
                        nx, ny, P, dx * dx, dy * dy, dy);
     CFDJ_HIP(hipGetLastError());
@@ -1014,6 +1018,33 @@ struct cfdj_cavity {
 
   // lid_driven_cavity.jl:75-114; rms of step k into d_rms[k]
   void step(double dt, int k) {
+    if (use_dst && poisson == CFDJ_CAVITY_DST) {
+      // the three solves write the other psi buffer (its boundary equals sn's: upload),
+      // so the previous step's psi survives for the RMS without a copy; the last row pass
+      // leaves the per-workgroup sums of (psi_new - psi_old)^2
+      double* A = sn;
+      double* B = sp;
+      stage(1, wn, wa, dt, A);
+      bc2(wa, A);
+      DstPoissonArgs a = dst_args(wa, B);
+      for (int pass = 0; pass < 3; ++pass) launch_dst_poisson_pass(pass, a, stream);
+      stage(2, wa, wb, dt, B);
+      bc2(wb, B);
+      a = dst_args(wb, B);
+      for (int pass = 0; pass < 3; ++pass) launch_dst_poisson_pass(pass, a, stream);
+      stage(3, wb, wn, dt, B);
+      bc2(wn, B);
+      a = dst_args(wn, B);
+      a.sprev = A;
+      a.part = part;
+      for (int pass = 0; pass < 3; ++pass) launch_dst_poisson_pass(pass, a, stream);
+      hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(256), 0, stream, part,
+                         dst_rows_grid(nx, ny, ncu), (double)(nx + 1) * (ny + 1), d_rms + k);
+      CFDJ_HIP(hipGetLastError());
+      sn = B;
+      sp = A;
+      return;
+    }
     CFDJ_HIP(hipMemcpyAsync(sp, sn, field() * sizeof(double), hipMemcpyDeviceToDevice, stream));
     stage(1, wn, wa, dt);  // wt = wn + dt r(wn, sn)
     bc2(wa);
@@ -1153,6 +1184,9 @@ int cfdj_cavity_upload(cfdj_cavity* h, const double* wn, long ldw, const double*
     select_device(h->device);
     copy_in(h->wn, h->P, wn, ldw, h->nx, h->ny, h->stream);
     copy_in(h->sn, h->P, sn, lds, h->nx, h->ny, h->stream);
+    // both psi buffers carry the caller's boundary values (the solves write interiors only)
+    CFDJ_HIP(hipMemcpyAsync(h->sp, h->sn, h->field() * sizeof(double), hipMemcpyDeviceToDevice,
+                            h->stream));
     CFDJ_HIP(hipStreamSynchronize(h->stream));
   });
 }

@@ -182,8 +182,13 @@ struct DstPoissonArgs {
   const double2* twX;  // exp(-2 pi i k / (2nx))
   const double2* twY;  // exp(-2 pi i k / (2ny))
   int ncu;
+  // optional (pass 2): per-workgroup sums of (s - sprev)^2 over the interior into part[0 ..
+  // dst_rows_grid(nx, ny, ncu))
+  const double* sprev;
+  double* part;
 };
 bool dst_poisson_supported(int nx, int ny);
+int dst_rows_grid(int nx, int ny, int ncu);
 void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
 
 // FFT-fused stage kernel (vm_fused.hip): row c2r of the column-pass output HA (rotated

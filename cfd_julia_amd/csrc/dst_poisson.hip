@@ -116,10 +116,15 @@ __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_fwd_kernel(
   }
 }
 
+// sprev / part (optional): this workgroup's sum of (s_new - sprev)^2 over the nodes it
+// writes goes to part[blockIdx.x] (fixed order: per-thread running sums, then a tree), the
+// first pass of the step's RMS of the streamfunction change (lid_driven_cavity.jl:112-114)
+// without re-reading both fields.
 template <int M2>
 __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
     const double2* __restrict__ T, int JT, double* __restrict__ s, int P, int ny,
-    const double2* __restrict__ tw_) {
+    const double2* __restrict__ tw_, const double* __restrict__ sprev,
+    double* __restrict__ part) {
   using PL = Plan<M2>;
   using C = DstRowCfg<M2>;
   constexpr int nx = M2 / 2;
@@ -130,7 +135,7 @@ __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
   double2* buf = lds + q * PL::PAD;
   const Range rg = persistent_range(blockIdx.x, gridDim.x, ny / C::ROWS);
   tw.fill(tw_);
-  if (rg.count <= 0) return;
+  double acc = 0.0;
   auto load_entries = [&](double2 (&e)[C::ENTRIES], int slot0) {
     const double2* tb = T + __builtin_amdgcn_readfirstlane(slot0);
     int tx = threadIdx.x;
@@ -143,7 +148,7 @@ __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
     }
   };
   double2 nxt[C::ENTRIES];
-  load_entries(nxt, rg.first * C::ROWS);
+  if (rg.count > 0) load_entries(nxt, rg.first * C::ROWS);
   __syncthreads();
   for (int it = 0; it < rg.count; ++it) {
     const int slot0 = (rg.first + it * rg.stride) * C::ROWS;
@@ -178,11 +183,32 @@ __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
       for (int r = 0; r < RL; ++r) {
         const int p = out_pos<M2, SL>(tid, b, r);
         if (p >= 1 && p < nx) {
-          if (oka) sa[p] = -v[b * RL + r].y;
-          if (okb) sb[p] = v[b * RL + r].x;
+          const double va = -v[b * RL + r].y, vb = v[b * RL + r].x;
+          if (oka) sa[p] = va;
+          if (okb) sb[p] = vb;
+          if (sprev != nullptr) {
+            if (oka) {
+              const double d = va - sprev[(size_t)ja * P + p];
+              acc += d * d;
+            }
+            if (okb) {
+              const double d = vb - sprev[(size_t)(ja + 1) * P + p];
+              acc += d * d;
+            }
+          }
         }
       }
     __syncthreads();  // LDS is rewritten by the next item
+  }
+  if (part != nullptr) {
+    double* red = reinterpret_cast<double*>(lds);
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = C::THREADS / 2; off > 0; off >>= 1) {
+      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
   }
 }
 
@@ -252,18 +278,24 @@ __global__ __launch_bounds__(Plan<M2>::T) void dst_cols_kernel(double2* __restri
 }
 
 template <int M2>
+int dst_rows_grid_t(int ny, int ncu) {
+  using C = DstRowCfg<M2>;
+  int nb = ncu - ncu % 8;
+  if (nb < 8) nb = 8;
+  const int items = ny / C::ROWS;
+  return nb < items ? nb : items;
+}
+
+template <int M2>
 void launch_dst_rows(int pass, const DstPoissonArgs& a, hipStream_t st) {
   using C = DstRowCfg<M2>;
-  int nb = a.ncu - a.ncu % 8;
-  if (nb < 8) nb = 8;
-  const int items = a.ny / C::ROWS;
-  const dim3 grid(nb < items ? nb : items);
+  const dim3 grid(dst_rows_grid_t<M2>(a.ny, a.ncu));
   if (pass == 0)
     hipLaunchKernelGGL((dst_rows_fwd_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.w, a.P, a.ny,
                        a.T, a.JT, a.neg ? -1.0 : 1.0, a.twX);
   else
     hipLaunchKernelGGL((dst_rows_inv_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.T, a.JT, a.s,
-                       a.P, a.ny, a.twX);
+                       a.P, a.ny, a.twX, a.sprev, a.sprev ? a.part : nullptr);
 }
 
 template <int M2>
@@ -278,6 +310,15 @@ constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
 bool dst_poisson_supported(int nx, int ny) {
   return pow2(nx) && pow2(ny) && nx >= 512 && nx <= 4096 && ny >= 512 && ny <= 4096;
+}
+
+int dst_rows_grid(int nx, int ny, int ncu) {
+  switch (2 * nx) {
+    case 1024: return dst_rows_grid_t<1024>(ny, ncu);
+    case 2048: return dst_rows_grid_t<2048>(ny, ncu);
+    case 4096: return dst_rows_grid_t<4096>(ny, ncu);
+    default: return dst_rows_grid_t<8192>(ny, ncu);
+  }
 }
 
 void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st) {
