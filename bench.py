@@ -46,10 +46,7 @@ STEP_BYTES_PER_CELL = 184
 # per-kernel algorithmic bytes per cell for cfdj_vm_kernel_bench ids:
 # stages read w (+ wn) and psi and write the stage output; each fused Poisson pass reads
 # and writes 8 B per cell (real field or half spectrum)
-# FFT-fused stage kernels (vm_fused.hip) read the column-pass spectrum 8 + omega_s 8
-# (+ omega^n 8) and write omega_out 8 + the next row spectrum 8; 10 = the column pass
-# writing the rotated layout they read
-KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16, 7: 32, 8: 40, 9: 40, 10: 16}
+KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16}
 KB_LAUNCHES = 20
 # Grid ladders (nx, ny) per GPU count; the second field of each value is the `scaling` label
 # of the runs at N > 1.  "c5" (default): BASELINE config 3 at N = 1, config 5 (8192^2) on
@@ -151,8 +148,6 @@ def main():
                     help="one-GPU rehearsal: RCCL slab code with a one-rank communicator")
     ap.add_argument("--poisson", default="auto", choices=["auto", "fused", "rocfft", "schur"])
     ap.add_argument("--rows-per-wave", type=int, default=None)
-    ap.add_argument("--no-fused-stage", action="store_true",
-                    help="five-pass stage sequence instead of the FFT-fused stage kernel")
     ap.add_argument("--ladder", default="c5", choices=sorted(LADDERS),
                     help="grid per GPU count (default: config 3 at N=1, config 5 at N>1)")
     ap.add_argument("--weak", action="store_const", const="weak", dest="ladder")
@@ -215,8 +210,6 @@ def main():
     else:
         h = VortexMerger(nx, ny, dx, dy, re, device=local_rank)
     h.set_poisson(args.poisson)
-    if args.no_fused_stage:
-        h.set_fused_stage(False)
     if args.rows_per_wave:
         h.set_rows_per_wave(args.rows_per_wave)
 
@@ -288,14 +281,12 @@ def main():
     value = cells * args.steps / elapsed / 1e6
     ms_step = elapsed * 1e3 / max(args.steps, 1)
     local_cells = cells / n_gpus
-    fstage = h.fused_stage()
-    kname = "vm_fused_stage_kernel" if fstage else "vm_stage_kernel"
+    kname = "vm_stage_kernel"
     # Roofline of the stage kernels from their IN-STEP launch times: HIP events around every
     # stage-kernel launch of the instrumented timed region (the kernels run in the step's
     # own sequence, between the Poisson passes), algorithmic bytes 24 / 32 / 32 per cell
-    # (FFT-fused: 32 / 40 / 40).  The back-to-back microbenchmark figure is kept beside it
-    # as frac_isolated.
-    alg_cell = (32, 40, 40) if fstage else (24, 32, 32)
+    # The back-to-back microbenchmark figure is kept beside it as frac_isolated.
+    alg_cell = (24, 32, 32)
     per_stage = []
     for i, (ms_i, n_i) in enumerate(kern_stage):
         if n_i:
@@ -319,9 +310,7 @@ def main():
         iso_alg = sum(k["alg_bytes"] for k in st) / 3.0
         iso = iso_alg / (iso_us * 1e-6) / 1e9
     roofline = {
-        "kernel": ("vm_fused_stage_kernel (row c2r of psi-hat + Arakawa J + 5-pt Laplacian "
-                   "+ RK3 stage + row r2c of the output, psi on chip)" if fstage else
-                   "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)"),
+        "kernel": "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)",
         "bound": "hbm",
         "achieved": round(stage_gbs, 1) if stage_gbs else None,
         "peak": HBM_PEAK_GBS,
@@ -362,7 +351,6 @@ def main():
                                f"Poisson + SSP-RK3 (vm.jl): {ladder_note}",
                    "nx": nx, "ny": ny, "dt": dt,
                    "re": re, "parallelism": parallelism, "poisson": h.poisson(),
-                   "fused_stage": fstage,
                    "cells_per_gpu": cells // n_gpus},
         "ms_per_step_instrumented": round(elapsed_i * 1e3 / args.steps, 4) if elapsed_i else None,
         "achieved_hbm_gbs_step": round(step_gbs, 1),

@@ -23,9 +23,7 @@ K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
 # cfdj_vm_kernel_bench kernel ids (CFDJ_KB_*)
 KB_NAMES = {1: "vm_stage_kernel<1>", 2: "vm_stage_kernel<2>", 3: "vm_stage_kernel<3>",
-            4: "rows_fwd_kernel", 5: "cols_kernel", 6: "rows_inv_kernel",
-            7: "vm_fused_stage_kernel<1>", 8: "vm_fused_stage_kernel<2>",
-            9: "vm_fused_stage_kernel<3>", 10: "cols_kernel(rot)"}
+            4: "rows_fwd_kernel", 5: "cols_kernel", 6: "rows_inv_kernel"}
 POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED, POISSON_SCHUR = 0, 1, 2, 3
 SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1
 CAVITY_DST, CAVITY_MG = 0, 1
@@ -84,8 +82,6 @@ SIGNATURES = {
     "cfdj_vm_slab": (C.c_int, [_vp, _ip, _ip]),
     "cfdj_vm_set_rows_per_wave": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_set_graph": (C.c_int, [_vp, C.c_int]),
-    "cfdj_vm_set_fused_stage": (C.c_int, [_vp, C.c_int]),
-    "cfdj_vm_get_fused_stage": (C.c_int, [_vp]),
     "cfdj_vm_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_get_poisson": (C.c_int, [_vp]),
     "cfdj_fps_set_poisson": (C.c_int, [_vp, C.c_int]),

@@ -142,10 +142,6 @@ struct cfdj_vm {
   double2* spec = nullptr;                                       // Single
   Fused fused;                                                   // Single, 2^k grids
   bool use_fused = false;
-  // FFT-fused stage kernel (vm_fused.hip): single-GPU fused-Poisson handles, nx <= 4096;
-  // specB is the second (natural-layout) row spectrum, spec the column-pass output
-  bool fuse_stage = false;  // opt-in until it outruns the five-pass sequence
-  double2* specB = nullptr;
   // substructured y-slab solve (schur.hip): traces of all ranks T, gathered column G
   SchurTables schur;
   bool use_schur = false;
@@ -598,9 +594,7 @@ struct cfdj_vm {
   double kernel_bench(int kernel, double dt, int n) {
     CFDJ_REQUIRE(mode == Mode::Single && use_fused,
                  "kernel bench needs a single-GPU handle on the fused Poisson path");
-    CFDJ_REQUIRE(kernel >= CFDJ_KB_STAGE1 && kernel <= CFDJ_KB_COLS_ROT, "bad kernel id");
-    CFDJ_REQUIRE(kernel < CFDJ_KB_FSTAGE1 || fused_stage_supported(nx, ny),
-                 "the FFT-fused stage kernel needs power-of-two nx 1024..4096");
+    CFDJ_REQUIRE(kernel >= CFDJ_KB_STAGE1 && kernel <= CFDJ_KB_ROWS_INV, "bad kernel id");
     CFDJ_REQUIRE(n >= 1, "launches must be >= 1");
     Slab& s = slabs[0];
     const FusedPoissonArgs a = fused.args(sym, s.wn, s.psi, spec, true);
@@ -615,10 +609,6 @@ struct cfdj_vm {
           case CFDJ_KB_STAGE1: launch_stage(1, stage_params(s, s.wn, s.wn, s.wa, dt), stream); break;
           case CFDJ_KB_STAGE2: launch_stage(2, stage_params(s, s.wa, s.wn, s.wb, dt), stream); break;
           case CFDJ_KB_STAGE3: launch_stage(3, stage_params(s, s.wb, s.wn, s.wn, dt), stream); break;
-          case CFDJ_KB_FSTAGE1: launch_fused_stage(1, fused_stage_params(s.wn, s.wa, dt, true), stream); break;
-          case CFDJ_KB_FSTAGE2: launch_fused_stage(2, fused_stage_params(s.wa, s.wb, dt, true), stream); break;
-          case CFDJ_KB_FSTAGE3: launch_fused_stage(3, fused_stage_params(s.wb, s.wn, dt, true), stream); break;
-          case CFDJ_KB_COLS_ROT: launch_fused_poisson_pass(1, fused_stage_cols(), stream); break;
           default: launch_fused_poisson_pass(kernel - CFDJ_KB_ROWS_FWD, a, stream); break;
         }
       }
@@ -635,68 +625,7 @@ struct cfdj_vm {
     return (double)t / n;
   }
 
-  bool fused_stage_active() const {
-    return fuse_stage && mode == Mode::Single && use_fused && !use_schur &&
-           fused_stage_supported(nx, ny);
-  }
-
-  FusedStageParams fused_stage_params(const double* w, double* out, double dt,
-                                      bool write_spec) const {
-    const StageParams sp = stage_params(slabs[0], w, slabs[0].wn, out, dt);
-    FusedStageParams f;
-    f.HA = spec;
-    f.HB = specB;
-    f.w = w;
-    f.wn = slabs[0].wn;
-    f.out = out;
-    f.twL = fused.twL;
-    f.twN = fused.twN;
-    f.nx = nx;
-    f.ny = ny;
-    f.band = fused_stage_band(nx, ny, fused.ncu);
-    f.write_spec = write_spec ? 1 : 0;
-    f.k = sp.k;
-    return f;
-  }
-
-  // Column-pass arguments of the fused-stage step: reads HB (natural), writes HA rotated.
-  FusedPoissonArgs fused_stage_cols() const {
-    FusedPoissonArgs c = fused.args(sym, slabs[0].wn, slabs[0].psi, specB, true);
-    c.Cout = spec;
-    c.rot = 1;
-    return c;
-  }
-
-  // nsteps RK3 steps with the FFT-fused stage kernel: one row r2c of omega^n, then per
-  // stage the column pass and the fused kernel (which leaves the next stage's row
-  // spectrum in specB).  psi is not materialised in HBM.
-  void steps_fused_stage(double dt, int nsteps) {
-    Slab& s = slabs[0];
-    CFDJ_REQUIRE(specB != nullptr, "fused stage: spectrum buffer missing");
-    tbegin(CFDJ_K_FFT_FWD);
-    launch_fused_poisson_pass(0, fused.args(sym, s.wn, s.psi, specB, true), stream);
-    tend();
-    const FusedPoissonArgs c = fused_stage_cols();
-    for (int n = 0; n < nsteps; ++n) {
-      for (int st = 1; st <= 3; ++st) {
-        const double* src = st == 1 ? s.wn : st == 2 ? s.wa : s.wb;
-        double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
-        tbegin(CFDJ_K_DIVIDE);
-        launch_fused_poisson_pass(1, c, stream);
-        tend();
-        tbegin(CFDJ_K_STAGE, st);
-        launch_fused_stage(st, fused_stage_params(src, out, dt, !(n == nsteps - 1 && st == 3)),
-                           stream);
-        tend();
-      }
-    }
-  }
-
   void steps_eager(double dt, int nsteps) {
-    if (fused_stage_active()) {
-      steps_fused_stage(dt, nsteps);
-      return;
-    }
     for (int n = 0; n < nsteps; ++n) {
       stage(1, dt);
       stage(2, dt);
@@ -825,10 +754,6 @@ struct cfdj_vm {
       }
       alloc_colparts();
     }
-    // second row spectrum of the FFT-fused stage (allocated up front: never inside a
-    // graph capture)
-    if (mode == Mode::Single && fused_stage_supported(nx, ny))
-      specB = dalloc<double2>((size_t)(nx / 2) * ny);
   }
 
   ~cfdj_vm() {
@@ -842,7 +767,6 @@ struct cfdj_vm {
     dfree(T);
     dfree(G);
     dfree(spec);
-    dfree(specB);
     dfree(gather);
     dfree(d_flag);
     for (auto e : ev) (void)hipEventDestroy(e);
@@ -1300,21 +1224,6 @@ int cfdj_vm_set_poisson(cfdj_vm* h, int path) {
     h->use_schur = sc;
     h->invalidate_graph();
   });
-}
-
-int cfdj_vm_set_fused_stage(cfdj_vm* h, int enable) {
-  return guard([&] {
-    CFDJ_REQUIRE(h != nullptr, "NULL handle");
-    select_device(h->device);
-    CFDJ_HIP(hipStreamSynchronize(h->stream));
-    h->fuse_stage = enable != 0;
-    h->invalidate_graph();
-  });
-}
-
-int cfdj_vm_get_fused_stage(cfdj_vm* h) {
-  if (!h) return CFDJ_ERR_ARG;
-  return h->fused_stage_active() ? 1 : 0;
 }
 
 int cfdj_vm_set_graph(cfdj_vm* h, int enable) {

@@ -144,9 +144,6 @@ struct FusedPoissonArgs {
   double2* C;           // column-pass buffer (kb columns of ny)
   double2* Cout;        // column-pass output (nullptr: in place into C)
   int tile8;            // row passes: spectrum in 8-mode tiles (Schur y-slab path)
-  int rot;              // column-pass output rotated: element y stored at (y - rot) mod ny
-                        // (one GPU only; the FFT-fused stage kernel reads row pairs
-                        // y+1, y+2 as one aligned segment, vm_fused.hip)
   int m0, kb;           // first global column and column count of C
   int rl_log2;          // log2(rows per column segment of C)
   unsigned seg;         // elements between the segments of one column of C
@@ -190,26 +187,6 @@ struct DstPoissonArgs {
 bool dst_poisson_supported(int nx, int ny);
 int dst_rows_grid(int nx, int ny, int ncu);
 void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
-
-// FFT-fused stage kernel (vm_fused.hip): row c2r of the column-pass output HA (rotated
-// layout: row y at (y - 1) mod ny) -> psi in LDS -> Arakawa + RK3 stage -> omega_out (HBM)
-// -> row r2c -> HB (natural layout), one GPU, power-of-two nx 1024..4096, ny 1024..8192.
-struct FusedStageParams {
-  const double2* HA;   // column-pass output (L x ny, column-major, rotated by one)
-  double2* HB;         // next stage's row spectrum (L x ny, column-major, natural)
-  const double* w;     // stencil input omega_s (pitch nx)
-  const double* wn;    // omega^n (stages 2 and 3)
-  double* out;         // stage output
-  const double2* twL;  // exp(-2 pi i k/(nx/2))
-  const double2* twN;  // exp(-2 pi i k/nx)
-  int nx, ny;
-  int band;            // rows per workgroup (fused_stage_band)
-  int write_spec;      // 0: skip the r2c of the output (last stage of a call)
-  StageCoef k;
-};
-bool fused_stage_supported(int nx, int ny);
-int fused_stage_band(int nx, int ny, int ncu);
-void launch_fused_stage(int stage, const FusedStageParams& p, hipStream_t st);
 
 // Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row

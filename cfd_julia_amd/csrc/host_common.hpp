@@ -267,7 +267,6 @@ struct Fused {
     a.H = H;
     a.C = C;
     a.Cout = nullptr;
-    a.rot = 0;
     a.tile8 = 0;
     a.kb = (nx / 2) / nranks;
     a.m0 = rank * a.kb;

@@ -192,7 +192,6 @@ struct DivArgs {
   int m0;         // global index of this buffer's first column (y-slabs: rank * L/P)
   int rl_log2;    // rows per segment (y-slabs: rows per rank; one GPU: M)
   unsigned seg;   // elements between the segments of one column (y-slabs: (L/P) * rows)
-  int rot;        // output element y goes to (y - rot) mod M (one GPU only; 0 = natural)
 };
 
 // v / d as v * (1/d) (recip_nr: the divide is the column pass's costliest step), for the
@@ -306,8 +305,7 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(const double2* __restr
   for (int b = 0; b < 16 / RL; ++b)
 #pragma unroll
     for (int r = 0; r < RL; ++r)
-      ocol[col_off((out_pos<M, SL>(tid, b, r) - da.rot) & (M - 1), da.rl_log2, da.seg)] =
-          v[b * RL + r];
+      ocol[col_off(out_pos<M, SL>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
 }
 
 // ---------------------------------------------------------------------------------------
@@ -467,7 +465,7 @@ void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st) {
 template <int M>
 void launch_cols(const FusedPoissonArgs& a, hipStream_t st) {
   DivArgs da{a.cx,  a.cy,  a.cy_mirror,        a.aa, a.bb, a.cc,       a.scale,
-             a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg, a.rot};
+             a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg};
   double2* out = a.Cout ? a.Cout : a.C;
   if (a.cy_mirror == nullptr)
     hipLaunchKernelGGL((cols_kernel<M, false>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, out, a.twM, da);
@@ -493,8 +491,7 @@ bool fused_poisson_supported(int nx, int ny, int rows) {
 
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st) {
   const bool ok = pass == 1 ? !a.tile8 && fused_poisson_supported(a.nx, a.ny, a.rows) && a.kb >= 1 &&
-                                 (1 << a.rl_log2) <= a.ny &&
-                                 (a.rot == 0 || (1 << a.rl_log2) == a.ny)
+                                 (1 << a.rl_log2) <= a.ny
                            : fused_rows_supported(a.nx, a.rows);
   if (!ok) throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
   if (pass == 1) {

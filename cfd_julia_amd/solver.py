@@ -189,15 +189,6 @@ class VortexMerger:
         check(_lib.load().cfdj_vm_set_rows_per_wave(self._h, int(rows)),
               "cfdj_vm_set_rows_per_wave")
 
-    def set_fused_stage(self, enable=True):
-        """FFT-fused stage kernel on/off (cfdj_vm_set_fused_stage)."""
-        check(_lib.load().cfdj_vm_set_fused_stage(self._h, int(bool(enable))),
-              "cfdj_vm_set_fused_stage")
-
-    def fused_stage(self):
-        """True when cfdj_vm_step runs the FFT-fused stage kernel."""
-        return _lib.load().cfdj_vm_get_fused_stage(self._h) == 1
-
     def set_graph(self, enable=True):
         check(_lib.load().cfdj_vm_set_graph(self._h, int(bool(enable))), "cfdj_vm_set_graph")
 

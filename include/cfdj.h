@@ -158,10 +158,6 @@ int cfdj_vm_stage_timing(cfdj_vm* h, double* ms3, long* launches3);
 #define CFDJ_KB_ROWS_FWD 4 /* fused Poisson pass 1: row r2c FFT */
 #define CFDJ_KB_COLS 5     /* fused Poisson pass 2: column FFT + divide + inverse FFT */
 #define CFDJ_KB_ROWS_INV 6 /* fused Poisson pass 3: row c2r FFT */
-#define CFDJ_KB_FSTAGE1 7  /* vm_fused_stage_kernel<1>: row c2r + stage 1 + row r2c */
-#define CFDJ_KB_FSTAGE2 8  /* vm_fused_stage_kernel<2> */
-#define CFDJ_KB_FSTAGE3 9  /* vm_fused_stage_kernel<3> */
-#define CFDJ_KB_COLS_ROT 10 /* column pass writing the rotated layout the fused stage reads */
 int cfdj_vm_kernel_bench(cfdj_vm* h, int kernel, double dt, int launches,
                          double* ms_per_launch);
 /* Optional finiteness check of the vorticity after each cfdj_vm_step call. */
@@ -175,12 +171,6 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
 /* Replay cfdj_vm_step's kernel sequence from a captured HIP graph (default on; used on
  * single-GPU handles with the fused Poisson path, others launch eagerly). */
 int cfdj_vm_set_graph(cfdj_vm* h, int enable);
-/* FFT-fused stage kernel (opt-in; used where supported: single GPU, fused Poisson path,
- * power-of-two nx 1024..4096): the row c2r, the Arakawa/RK3 stage and the next stage's
- * row r2c in one kernel per stage (psi stays on chip).  Off: the five-pass sequence.
- * get returns 1 when the fused stage is in use for cfdj_vm_step, 0 if not. */
-int cfdj_vm_set_fused_stage(cfdj_vm* h, int enable);
-int cfdj_vm_get_fused_stage(cfdj_vm* h);
 /* Select / query the Poisson implementation (CFDJ_POISSON_*; single-GPU and slab handles). */
 int cfdj_vm_set_poisson(cfdj_vm* h, int path);
 int cfdj_vm_get_poisson(cfdj_vm* h);

@@ -10,5 +10,5 @@ h = VortexMerger(n, n, dx, dx, 1000.0, device=0)
 x = dx * np.arange(n + 1)
 wn = np.zeros((n + 2, n + 2), order="F"); vm_ic(n, n, x, x, wn); h.upload(wn)
 h.step(5e-4, 1)
-for k in [int(i) for i in os.environ.get("KB_IDS", "7,8,9").split(",")]:
+for k in [int(i) for i in os.environ.get("KB_IDS", "1,2,3,4,5,6").split(",")]:
     print(k, round(h.kernel_bench(k, 5e-4, int(os.environ.get("KB_N", "3"))) * 1e3, 1))

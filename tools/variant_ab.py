@@ -1,6 +1,6 @@
 """Per-launch time of step kernels (cfdj_vm_kernel_bench ids in $KB_IDS, default 1-6) for each
 libcfdj variant given on the command line (built by tools/build_variant.sh); one process
-per variant.  python tools/fstage_ab.py build/a/libcfdj.so build/b/libcfdj.so ..."""
+per variant.  python tools/variant_ab.py build/a/libcfdj.so build/b/libcfdj.so ..."""
 import json, os, subprocess, sys
 
 CODE = r'''
