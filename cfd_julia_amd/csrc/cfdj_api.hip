@@ -133,6 +133,7 @@ struct cfdj_vm {
   double dx = 0, dy = 0, re = 0, eps = 0;
   int device = -1;
   int rows_per_wave = 16;
+  bool stage_march = false;  // set by cfdj_vm_set_rows_per_wave: marching stage kernel only
   hipStream_t stream = nullptr;
   std::vector<Slab> slabs;
   Symbol sym;
@@ -505,6 +506,7 @@ struct cfdj_vm {
     p.ycount = rows;
     p.colpart = nullptr;
     p.rows_per_wave = rows_per_wave;
+    p.march = stage_march;
     const double dx2 = dx * dx, dy2 = dy * dy;
     p.k.aa = 1.0 / (re * dx2);
     p.k.bb = 1.0 / (re * dy2);
@@ -1202,6 +1204,7 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
     select_device(h->device);
     CFDJ_HIP(hipStreamSynchronize(h->stream));
     h->rows_per_wave = rows;
+    h->stage_march = true;
     if (h->use_schur) h->alloc_colparts();  // partial blocks follow the wave row ranges
     h->invalidate_graph();
   });

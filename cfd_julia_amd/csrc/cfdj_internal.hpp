@@ -92,6 +92,7 @@ struct StageParams {
   int y0, ycount;      // rows [y0, y0 + ycount) of the slab are computed (halo split)
   double* colpart;     // optional: per-wave column sums of `out`, [y / rows_per_wave][nx]
   int rows_per_wave;
+  bool march;          // true: always the marching kernel (rows_per_wave rows per wavefront)
   StageCoef k;
 };
 

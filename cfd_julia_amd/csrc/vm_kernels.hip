@@ -101,6 +101,133 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
     *reinterpret_cast<double2*>(p.colpart + (size_t)(ybeg / p.rows_per_wave) * nx + xs) = csum;
 }
 
+// Row-group variant of the stage kernel: a 256-thread workgroup owns 512 consecutive x of
+// kTileRows consecutive rows (two x per lane, every row of the group and its two halo rows
+// loaded at once, 16 B per lane), instead of a wavefront marching down 32 rows.  Workgroups
+// run in row-major order, so at any moment the chip works on one narrow band of rows: the
+// three or four streams (omega_s, psi, omega^n, output) advance through HBM sequentially,
+// which the memory system serves 14-18 % faster than the marching kernels' 128 scattered
+// row fronts (6.1 against 5.0-5.3 TB/s for the bare access shapes, tools/micro/streambench).
+// The halo rows a group shares with its neighbours are re-read through L2: the group above
+// and below are workgroups b -/+ nx/512, which land on the same XCD for nx = 4096.
+// x-neighbours: lane shuffles; across wavefronts of the workgroup through LDS; at the
+// workgroup's two edges one masked load per row and field.  Same arithmetic (stencil.hpp).
+#ifndef CFDJ_TILE_ROWS
+#define CFDJ_TILE_ROWS 2
+#endif
+#ifndef CFDJ_TILE_WAVES
+#define CFDJ_TILE_WAVES 0  // > 0: occupancy target in wavefronts per SIMD (register cap)
+#endif
+#if CFDJ_TILE_WAVES > 0
+#define CFDJ_TILE_ATTR __attribute__((amdgpu_waves_per_eu(CFDJ_TILE_WAVES, CFDJ_TILE_WAVES)))
+#else
+#define CFDJ_TILE_ATTR
+#endif
+constexpr int kTileRows = CFDJ_TILE_ROWS;
+constexpr int kTileCols = 512;
+constexpr int kXcds = 8;  // MI355X: workgroup b is dispatched to XCD b % 8
+
+template <int STAGE>
+__global__ __launch_bounds__(256) CFDJ_TILE_ATTR void vm_stage_tile_kernel(const StageParams p) {
+  constexpr int G = kTileRows, NR = G + 2, NW = 256 / kWave;
+  // left[w]: the value left of wavefront w's first x (w = 0: the workgroup's halo column);
+  // right[w]: the value right of its last x (w = NW - 1: the halo column); per row and field
+  __shared__ double left[NW][2 * NR], right[NW][2 * NR];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nx = p.nx, ny = p.ny;
+  const int strips = nx / kTileCols;
+  // Workgroup b runs on XCD b % 8.  A row group shares its halo rows with the groups above
+  // and below, so those should sit on the same XCD (one L2): automatic when the strip count
+  // is a multiple of 8; for 1, 2 or 4 strips the rows are split into 8 / strips bands and
+  // XCD (strip, band) walks its band.
+  int strip = blockIdx.x % strips, grp = blockIdx.x / strips;
+  if (strips < kXcds && kXcds % strips == 0) {
+    const int bands = kXcds / strips, ngrp = p.ycount / G;
+    if (ngrp % bands == 0) {
+      const int xcd = blockIdx.x % kXcds, i = blockIdx.x / kXcds;
+      strip = xcd % strips;
+      grp = (xcd / strips) * (ngrp / bands) + i;
+    }
+  }
+  const int x0 = strip * kTileCols;
+  const int x = x0 + 2 * (int)threadIdx.x;
+  const int y0 = p.y0 + grp * G;
+
+  double2 wv[NR], sv[NR], wnv[G];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const double* wr = row_ptr(p.w, p.w_lo, p.w_hi, y0 - 1 + j, ny, nx);
+    const double* sr = row_ptr(p.s, p.s_lo, p.s_hi, y0 - 1 + j, ny, nx);
+    wv[j] = *reinterpret_cast<const double2*>(wr + x);
+    sv[j] = *reinterpret_cast<const double2*>(sr + x);
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    wnv[j] = make_double2(0.0, 0.0);
+    if constexpr (STAGE >= 2)
+      wnv[j] = *reinterpret_cast<const double2*>(p.wn + (size_t)(y0 + j) * nx + x);
+  }
+  // The two halo columns of the workgroup (periodic in x): one load in the first
+  // wavefront, lane i < 4 NR fetching (side, row, field) = (i / 2NR, (i % 2NR) / 2, i % 2).
+  static_assert(4 * NR <= kWave, "halo fetch needs one lane per value");
+  double halo = 0.0;
+  if (threadIdx.x < 4 * NR) {
+    const int side = threadIdx.x / (2 * NR), rem = threadIdx.x % (2 * NR);
+    const int xh = side == 0 ? (x0 == 0 ? nx - 1 : x0 - 1)
+                             : (x0 + kTileCols >= nx ? x0 + kTileCols - nx : x0 + kTileCols);
+    const double* r = (rem & 1) ? row_ptr(p.s, p.s_lo, p.s_hi, y0 - 1 + rem / 2, ny, nx)
+                                : row_ptr(p.w, p.w_lo, p.w_hi, y0 - 1 + rem / 2, ny, nx);
+    halo = r[xh];
+  }
+  // Edge lanes publish one value per row and field: lane 0 its first x as the right
+  // neighbour of the wavefront before it, lane 63 its last x as the left neighbour of the
+  // wavefront after it.
+  if ((lane == 0 && wave > 0) || (lane == kWave - 1 && wave < NW - 1)) {
+    double* e = lane == 0 ? right[wave - 1] : left[wave + 1];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      e[2 * j] = lane == 0 ? wv[j].x : wv[j].y;
+      e[2 * j + 1] = lane == 0 ? sv[j].x : sv[j].y;
+    }
+  }
+  if (threadIdx.x < 4 * NR) {
+    const int side = threadIdx.x / (2 * NR), rem = threadIdx.x % (2 * NR);
+    (side == 0 ? left[0] : right[NW - 1])[rem] = halo;
+  }
+  __syncthreads();
+  const StageCoef k = p.k;
+  Win ww[NR], sw[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    ww[j].a = wv[j].x;
+    ww[j].b = wv[j].y;
+    sw[j].a = sv[j].x;
+    sw[j].b = sv[j].y;
+    ww[j].l = __shfl_up(wv[j].y, 1, kWave);
+    ww[j].r = __shfl_down(wv[j].x, 1, kWave);
+    sw[j].l = __shfl_up(sv[j].y, 1, kWave);
+    sw[j].r = __shfl_down(sv[j].x, 1, kWave);
+    if (lane == 0) {
+      ww[j].l = left[wave][2 * j];
+      sw[j].l = left[wave][2 * j + 1];
+    }
+    if (lane == kWave - 1) {
+      ww[j].r = right[wave][2 * j];
+      sw[j].r = right[wave][2 * j + 1];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    double r0, r1;
+    pair_rhs(ww[j], ww[j + 1], ww[j + 2], sw[j], sw[j + 1], sw[j + 2], k, r0, r1);
+    double2 o;
+    o.x = stage_update<STAGE>(r0, ww[j + 1].a, wnv[j].x, k);
+    o.y = stage_update<STAGE>(r1, ww[j + 1].b, wnv[j].y, k);
+    *reinterpret_cast<double2*>(p.out + (size_t)(y0 + j) * nx + x) = o;
+  }
+}
+
 // colpart[b][x] = sum over rows [b rpw, (b+1) rpw) of f[y][x], in the row order of the
 // stage kernel's csum (so a field gets the same partials either way).
 __global__ __launch_bounds__(256) void colpart_kernel(const double* __restrict__ f, int nx,
@@ -199,7 +326,30 @@ __global__ __launch_bounds__(256) void finite_kernel(const double* __restrict__ 
 
 }  // namespace
 
+// The row-group kernel where it applies: row length a multiple of 512, a row count that
+// is a multiple of the group, no column partial sums, and the caller has not asked for the
+// marching kernel.
+static bool stage_tile_ok(const StageParams& p) {
+  return !p.march && p.colpart == nullptr && p.nx % kTileCols == 0 &&
+         p.ycount % kTileRows == 0 && p.ycount > 0;
+}
+
 void launch_stage(int stage, const StageParams& p, hipStream_t st) {
+  if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
+    throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};
+  if (stage_tile_ok(p)) {
+    const long blocks = (long)(p.nx / kTileCols) * (p.ycount / kTileRows);
+    if (blocks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
+    const dim3 grid((unsigned)blocks), block(256);
+    switch (stage) {
+      case 0: hipLaunchKernelGGL(vm_stage_tile_kernel<0>, grid, block, 0, st, p); break;
+      case 1: hipLaunchKernelGGL(vm_stage_tile_kernel<1>, grid, block, 0, st, p); break;
+      case 2: hipLaunchKernelGGL(vm_stage_tile_kernel<2>, grid, block, 0, st, p); break;
+      default: hipLaunchKernelGGL(vm_stage_tile_kernel<3>, grid, block, 0, st, p); break;
+    }
+    CFDJ_HIP(hipGetLastError());
+    return;
+  }
   const int rpw = p.rows_per_wave;
   const long strips = (p.nx + kColsPerWave - 1) / kColsPerWave;
   if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)

@@ -166,7 +166,10 @@ int cfdj_vm_set_check_finite(cfdj_vm* h, int enable);
 int cfdj_vm_field_device(cfdj_vm* h, double** w_dev);
 /* Shape of this rank's slab: global row offset and row count. */
 int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows);
-/* Tuning: rows marched by one wavefront in the stage kernel (default chosen per size). */
+/* Tuning: select the marching stage kernel (one wavefront walks `rows` rows of a
+ * 128-column strip).  Without this call the row-group stage kernel runs wherever it applies
+ * (nx a multiple of 512, even row count, no column partial sums) and the marching kernel,
+ * with a rows-per-wavefront default chosen per size, elsewhere.  Results are bit-identical. */
 int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
 /* Replay cfdj_vm_step's kernel sequence from a captured HIP graph (default on; used on
  * single-GPU handles with the fused Poisson path, others launch eagerly). */

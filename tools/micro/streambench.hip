@@ -67,6 +67,75 @@ __global__ __launch_bounds__(256) void march_kernel(const double* __restrict__ a
   }
 }
 
+// march with a D-row-deep register prefetch ring
+template <int R, int D>
+__global__ __launch_bounds__(256) void march_deep_kernel(const double* __restrict__ a,
+                                                         const double* __restrict__ b,
+                                                         const double* __restrict__ c,
+                                                         double* __restrict__ o, int nx, int ny, int rpw) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int strips = nx / 128;
+  const int tile = blockIdx.x;
+  const int strip = tile % strips, chunk = tile / strips;
+  const int x = strip * 128 + 2 * lane;
+  const int y0 = (chunk * 4 + wave) * rpw;
+  double2 pa[D], pb[D], pc[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) {
+    pa[d] = *reinterpret_cast<const double2*>(a + (size_t)(y0 + d) * nx + x);
+    if (R >= 2) pb[d] = *reinterpret_cast<const double2*>(b + (size_t)(y0 + d) * nx + x);
+    if (R >= 3) pc[d] = *reinterpret_cast<const double2*>(c + (size_t)(y0 + d) * nx + x);
+  }
+  for (int yb = y0; yb < y0 + rpw; yb += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int y = yb + d;
+      const int yn = y + D < y0 + rpw ? y + D : y;
+      double2 r = pa[d];
+      if (R >= 2) { r.x += pb[d].x; r.y += pb[d].y; }
+      if (R >= 3) { r.x += pc[d].x; r.y += pc[d].y; }
+      pa[d] = *reinterpret_cast<const double2*>(a + (size_t)yn * nx + x);
+      if (R >= 2) pb[d] = *reinterpret_cast<const double2*>(b + (size_t)yn * nx + x);
+      if (R >= 3) pc[d] = *reinterpret_cast<const double2*>(c + (size_t)yn * nx + x);
+      *reinterpret_cast<double2*>(o + (size_t)y * nx + x) = r;
+    }
+  }
+}
+
+// row-group tile: a 256-thread workgroup covers 512 columns x G rows; every thread loads its
+// column pair of rows y0-1 .. y0+G of a and b (halo rows re-read through L1 / L2) and of rows
+// y0 .. y0+G-1 of c, writes G rows: the traffic shape of a stencil stage without marching.
+template <int R, int G>
+__global__ __launch_bounds__(256) void tile_kernel(const double* __restrict__ a,
+                                                   const double* __restrict__ b,
+                                                   const double* __restrict__ c,
+                                                   double* __restrict__ o, int nx, int ny) {
+  const int strips = nx / 512;
+  const int strip = blockIdx.x % strips, grp = blockIdx.x / strips;
+  const int x = strip * 512 + 2 * threadIdx.x;
+  const int y0 = grp * G;
+  double2 va[G + 2], vb[G + 2], vc[G];
+#pragma unroll
+  for (int j = 0; j < G + 2; ++j) {
+    const int y = (y0 - 1 + j + ny) % ny;
+    va[j] = *reinterpret_cast<const double2*>(a + (size_t)y * nx + x);
+    if (R >= 2) vb[j] = *reinterpret_cast<const double2*>(b + (size_t)y * nx + x);
+  }
+  if (R >= 3) {
+#pragma unroll
+    for (int j = 0; j < G; ++j) vc[j] = *reinterpret_cast<const double2*>(c + (size_t)(y0 + j) * nx + x);
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    double2 r;
+    r.x = va[j].x + va[j + 1].x + va[j + 2].x;
+    r.y = va[j].y + va[j + 1].y + va[j + 2].y;
+    if (R >= 2) { r.x += vb[j].x + vb[j + 1].x + vb[j + 2].x; r.y += vb[j].y + vb[j + 1].y + vb[j + 2].y; }
+    if (R >= 3) { r.x += vc[j].x; r.y += vc[j].y; }
+    *reinterpret_cast<double2*>(o + (size_t)(y0 + j) * nx + x) = r;
+  }
+}
+
 int main(int argc, char** argv) {
   const int nx = argc > 1 ? atoi(argv[1]) : 4096, ny = argc > 2 ? atoi(argv[2]) : nx;
   printf("arrays of %d x %d doubles (%.0f MB each)\n", nx, ny, (double)nx * ny * 8 / 1e6);
@@ -110,5 +179,30 @@ int main(int argc, char** argv) {
     char nm[64]; snprintf(nm, 64, "march rows/wave=%d", RPW); report(nm, R, ms);              \
   }
   RUN_MARCH(1, 32) RUN_MARCH(2, 32) RUN_MARCH(3, 32) RUN_MARCH(2, 8) RUN_MARCH(3, 8) RUN_MARCH(2, 64) RUN_MARCH(3, 64)
+#define RUN_DEEP(R, D, RPW)                                                                   \
+  {                                                                                           \
+    const unsigned grid = (unsigned)((nx / 128) * (ny / (4 * RPW)));                          \
+    hipLaunchKernelGGL((march_deep_kernel<R, D>), dim3(grid), dim3(256), 0, 0, a, b, c, o, nx, ny, RPW); \
+    CK(hipEventRecord(e0));                                                                   \
+    for (int i = 0; i < reps; ++i)                                                            \
+      hipLaunchKernelGGL((march_deep_kernel<R, D>), dim3(grid), dim3(256), 0, 0, a, b, c, o, nx, ny, RPW); \
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));                                      \
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));                                           \
+    char nm[64]; snprintf(nm, 64, "march deep D=%d rows/wave=%d", D, RPW); report(nm, R, ms); \
+  }
+#define RUN_TILE(R, G)                                                                        \
+  {                                                                                           \
+    const unsigned grid = (unsigned)((nx / 512) * (ny / G));                                  \
+    hipLaunchKernelGGL((tile_kernel<R, G>), dim3(grid), dim3(256), 0, 0, a, b, c, o, nx, ny); \
+    CK(hipEventRecord(e0));                                                                   \
+    for (int i = 0; i < reps; ++i)                                                            \
+      hipLaunchKernelGGL((tile_kernel<R, G>), dim3(grid), dim3(256), 0, 0, a, b, c, o, nx, ny); \
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));                                      \
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));                                           \
+    char nm[64]; snprintf(nm, 64, "tile 512 x %d rows", G); report(nm, R, ms);                \
+  }
+  RUN_TILE(2, 2) RUN_TILE(2, 4) RUN_TILE(2, 8) RUN_TILE(3, 2) RUN_TILE(3, 4) RUN_TILE(3, 8) RUN_TILE(2, 1) RUN_TILE(3, 1)
+  RUN_DEEP(2, 2, 32) RUN_DEEP(2, 4, 32) RUN_DEEP(2, 8, 32) RUN_DEEP(3, 2, 32) RUN_DEEP(3, 4, 32) RUN_DEEP(3, 8, 32)
+  RUN_DEEP(2, 4, 16) RUN_DEEP(3, 4, 16) RUN_DEEP(2, 8, 64) RUN_DEEP(3, 8, 64)
   return 0;
 }
