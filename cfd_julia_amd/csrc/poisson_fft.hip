@@ -210,10 +210,37 @@ __device__ __forceinline__ double2 sym_apply(double2 v, double d, double d2, dou
   return make_double2(x * id, y * id);
 }
 
+// Element k of the packed column: Z = Z[k], Zp = Z[-k].  A = (Z + conj Zp)/2 belongs to the
+// kx = eps column, B = (Z - conj Zp)/(2i) to kx = -pi; each is divided by its own symbol
+// and the pair re-packed as A' + i B'.
+struct DivArgs;
+__device__ __forceinline__ double2 packed_divide(double2 Z, double2 Zp, int k, double ax,
+                                              double axL, const DivArgs& da, double sgn,
+                                              bool mirror);
+
 // Element y of a column: rows are stored in segments of 2^rl_log2 (one per source rank of
 // the y-slab all-to-all), `seg` elements apart; on one GPU the column is one segment.
 __device__ __forceinline__ unsigned col_off(int y, int rl_log2, unsigned seg) {
   return (unsigned)(y >> rl_log2) * seg + (unsigned)(y & ((1 << rl_log2) - 1));
+}
+
+__device__ __forceinline__ double2 packed_divide(double2 Z, double2 Zp, int k, double ax,
+                                              double axL, const DivArgs& da, double sgn,
+                                              bool mirror) {
+  const double2 Zc = cconj(Zp);
+  const double2 A = make_double2(0.5 * (Z.x + Zc.x), 0.5 * (Z.y + Zc.y));
+  const double2 D = csub(Z, Zc);
+  const double2 B = make_double2(0.5 * D.y, -0.5 * D.x);
+  const double cyk = da.cy[k];
+  const double cym = mirror ? da.cy_mirror[k] : cyk;
+  const double d0 = fd_symbol(ax, da.cc, cyk);   // kx = eps column
+  const double dL = fd_symbol(axL, da.cc, cyk);  // kx = -pi column
+  const double d0m = fd_symbol(ax, da.cc, cym);
+  const double dLm = fd_symbol(axL, da.cc, cym);
+  const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0 (Common.jl:118)
+                            : sym_apply(A, d0, d0m, sgn, mirror);
+  const double2 B2 = sym_apply(B, dL, dLm, sgn, mirror);
+  return make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
 }
 
 template <int M>
@@ -226,37 +253,30 @@ __device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __rest
     for (int r = 0; r < R0; ++r) a[b * R0 + r] = col[col_off(in_pos<M, 0>(tid, b, r), rl_log2, seg)];
 }
 
-template <int M, bool MIRROR>
-__global__ __launch_bounds__(Plan<M>::T) void cols_kernel(const double2* __restrict__ C,
-                                                        double2* __restrict__ Cout,
-                                                        const double2* __restrict__ twM_,
-                                                        const DivArgs da) {
-  // One column per workgroup (2 resident per CU at M = 4096): not persistent, because the
-  // divide's cy[k] loads would queue behind a next-column prefetch (vmcnt is in order).
+// One column: forward FFT, divide, inverse FFT.  PACKED = the column of slot 0, Z =
+// FFT_y(X_dc + i X_nyq): split with the partner Z[-k] into the DC and the Nyquist column,
+// each divided by its own symbol (kx = eps and kx = -pi), re-packed.  One workgroup in L
+// does this and it must not set the kernel's register count: it is a separate instantiation
+// of the whole body (no merge of two versions of the registers), its spectrum goes through
+// the output column in global memory and a rolled loop over the pairs (k, M - k) transforms
+// it in place.
+template <int M, bool MIRROR, bool PACKED>
+__device__ __forceinline__ void cols_column(double* lds, const double2* __restrict__ col,
+                                            double2* __restrict__ ocol, int m, int tid,
+                                            const TwGlobal<M>& twM, const DivArgs& da) {
   using P = Plan<M>;
-  static_assert(P::NSTAGES >= 2, "column length");
-  __shared__ double2 lds[P::PAD];
-  const TwGlobal<M> twM{twM_};
-  const int tid = threadIdx.x;
-  const int ml = xcd_remap(blockIdx.x, gridDim.x);
-  const int m = da.m0 + ml;  // global x-mode
   const double sgn = da.neg ? -1.0 : 1.0;
   constexpr bool mirror = MIRROR;  // symbol not even in ky (ny < nx): a template flag, so
                                   // the square-grid kernel carries no cy_mirror loads
-  const double2* col = C + ((size_t)ml << da.rl_log2);
-  double2* ocol = Cout + ((size_t)ml << da.rl_log2);
-
   double2 a[16];
   load_col<M>(a, col, tid, da.rl_log2, da.seg);
   stage_regs<M, 0, -1>(a, tid, twM);
-  lds_write<M, 0>(lds, a, tid);
-  __syncthreads();
-  run_stages<M, 1, -1, false>(lds, a, tid, twM);  // last stage stays in registers
+  run_stages_half<M, 1, -1>(lds, a, tid, twM);  // last stage stays in registers
 
   double2 v[16];
   fwd_to_inv<M>(a, v);  // v[r] = spectrum at k = tid + T*r, natural order
   const double ax = fd_symbol_x(da.aa, da.bb, da.cx[m]);
-  if (m != 0) {
+  if constexpr (!PACKED) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int k = tid + P::T * r;
@@ -266,38 +286,26 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(const double2* __restr
       v[r] = make_double2(q.x * da.scale, q.y * da.scale);
     }
   } else {
-    // packed column: Z = FFT_y(X_dc + i X_nyq); split with Z[-k], divide each half by its
-    // own symbol (kx = eps and kx = -pi), re-pack.  Partners come through LDS.
-    __syncthreads();  // all reads of the last forward stage are done
 #pragma unroll
-    for (int r = 0; r < 16; ++r) lds[padx(tid + P::T * r)] = v[r];
-    __syncthreads();
+    for (int r = 0; r < 16; ++r) ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)] = v[r];
+    __syncthreads();  // workgroup-scope release / acquire of the global stores
     const double axL = fd_symbol_x(da.aa, da.bb, da.cx[da.L]);
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int k = tid + P::T * r;
-      const double2 Z = v[r];
-      const double2 Zc = cconj(lds[padx((M - k) & (M - 1))]);
-      const double2 A = make_double2(0.5 * (Z.x + Zc.x), 0.5 * (Z.y + Zc.y));
-      const double2 D = csub(Z, Zc);
-      const double2 B = make_double2(0.5 * D.y, -0.5 * D.x);
-      const double cyk = da.cy[k];
-      const double cym = mirror ? da.cy_mirror[k] : cyk;
-      const double d0 = fd_symbol(ax, da.cc, cyk);   // kx = eps column
-      const double dL = fd_symbol(axL, da.cc, cyk);  // kx = -pi column
-      const double d0m = fd_symbol(ax, da.cc, cym);
-      const double dLm = fd_symbol(axL, da.cc, cym);
-      const double2 A2 = k == 0 ? make_double2(0.0, 0.0)  // e[1,1] = 0 (Common.jl:118)
-                                : sym_apply(A, d0, d0m, sgn, mirror);
-      const double2 B2 = sym_apply(B, dL, dLm, sgn, mirror);
-      v[r] = make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
+#pragma unroll 1
+    for (int k = tid; k <= M / 2; k += P::T) {
+      const int kp = (M - k) & (M - 1);
+      double2* pk = ocol + col_off(k, da.rl_log2, da.seg);
+      double2* pp = ocol + col_off(kp, da.rl_log2, da.seg);
+      const double2 Zk = *pk, Zq = *pp;
+      *pk = packed_divide(Zk, Zq, k, ax, axL, da, sgn, mirror);
+      if (kp != k) *pp = packed_divide(Zq, Zk, kp, ax, axL, da, sgn, mirror);
     }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)];
+    __syncthreads();  // every reload precedes the final stores to the same column
   }
-  __syncthreads();  // LDS is rewritten by the inverse stage 0
   stage_regs<M, 0, 1>(v, tid, twM);
-  lds_write<M, 0>(lds, v, tid);
-  __syncthreads();
-  run_stages<M, 1, 1, false>(lds, v, tid, twM);
+  run_stages_half<M, 1, 1>(lds, v, tid, twM);
   // last inverse stage: outputs j + r*NS are in natural order -> straight to HBM
   constexpr int SL = P::NSTAGES - 1;
   constexpr int RL = P::radix(SL);
@@ -306,6 +314,39 @@ __global__ __launch_bounds__(Plan<M>::T) void cols_kernel(const double2* __restr
 #pragma unroll
     for (int r = 0; r < RL; ++r)
       ocol[col_off(out_pos<M, SL>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
+}
+
+// Wavefronts per SIMD the column kernel is compiled for (its register cap): one per
+// resident workgroup when a workgroup is 4 wavefronts (M = 4096: LDS allows 4, registers 3).
+template <int M>
+constexpr int cols_waves() { return Plan<M>::T == 256 && M <= 4096 ? 3 : 2; }
+
+template <int M, bool MIRROR>
+__global__ __launch_bounds__(Plan<M>::T)
+    __attribute__((amdgpu_waves_per_eu(cols_waves<M>(), cols_waves<M>()))) void cols_kernel(const double2* __restrict__ C,
+                                                        double2* __restrict__ Cout,
+                                                        const double2* __restrict__ twM_,
+                                                        const DivArgs da) {
+  // One column per workgroup: not persistent, because the divide's cy[k] loads would queue
+  // behind a next-column prefetch (vmcnt is in order).  The workgroups of a CU overlap each
+  // other's memory and FFT phases instead, so their number matters: the LDS buffer holds one
+  // double per element and the stages exchange real and imaginary parts one after the other
+  // (exchange_half), 34 KB at M = 4096 -- three workgroups per CU (the registers' limit)
+  // where a complex buffer allows two.
+  using P = Plan<M>;
+  static_assert(P::NSTAGES >= 2, "column length");
+  __shared__ double lds[P::PAD];
+  const TwGlobal<M> twM{twM_};
+  const int tid = threadIdx.x;
+  const int ml = xcd_remap(blockIdx.x, gridDim.x);
+  const int m = da.m0 + ml;  // global x-mode
+  const double2* col = C + ((size_t)ml << da.rl_log2);
+  double2* ocol = Cout + ((size_t)ml << da.rl_log2);
+  if (m == 0) {
+    cols_column<M, MIRROR, true>(lds, col, ocol, m, tid, twM, da);
+    return;
+  }
+  cols_column<M, MIRROR, false>(lds, col, ocol, m, tid, twM, da);
 }
 
 // ---------------------------------------------------------------------------------------
