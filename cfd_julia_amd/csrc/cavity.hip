@@ -20,22 +20,47 @@ struct CavCoef {
   double aa, bb, gg, hh, dt, c25dt, c13, c23, c23dt;
 };
 
-// lid_driven_cavity.jl:124-159 at interior node (i, j); gg inside each term.
+// lid_driven_cavity.jl:124-159 at an interior node from its nine omega and eight psi
+// values (c = centre, E/W = i +- 1, N/S = j +- 1); gg inside each term.
+struct Nine {
+  double c, E, W, N, S, NE, SW, NW, SE;
+};
+__device__ __forceinline__ double cavity_rhs_vals(const Nine& w, const Nine& s,
+                                                  const CavCoef& k) {
+  const double j1 = k.gg * ((w.E - w.W) * (s.N - s.S) - (w.N - w.S) * (s.E - s.W));
+  const double j2 = k.gg * (w.E * (s.NE - s.SE) - w.W * (s.NW - s.SW) - w.N * (s.NE - s.NW) +
+                            w.S * (s.SE - s.SW));
+  const double j3 = k.gg * (w.NE * (s.N - s.E) - w.SW * (s.W - s.S) - w.NW * (s.N - s.W) +
+                            w.SE * (s.E - s.S));
+  const double jac = (j1 + j2 + j3) * k.hh;
+  return -jac + (k.aa * (w.E - 2.0 * w.c + w.W) + k.bb * (w.N - 2.0 * w.c + w.S));
+}
+__device__ __forceinline__ Nine nine_at(const double* __restrict__ a, size_t c, int P) {
+  Nine n;
+  n.c = a[c];
+  n.E = a[c + 1];
+  n.W = a[c - 1];
+  n.N = a[c + P];
+  n.S = a[c - P];
+  n.NE = a[c + P + 1];
+  n.SW = a[c - P - 1];
+  n.NW = a[c + P - 1];
+  n.SE = a[c - P + 1];
+  return n;
+}
 __device__ __forceinline__ double cavity_rhs_at(const double* __restrict__ w,
                                                 const double* __restrict__ s, size_t c,
                                                 int P, const CavCoef& k) {
-  const double wc = w[c];
-  const double wE = w[c + 1], wW = w[c - 1], wN = w[c + P], wS = w[c - P];
-  const double wNE = w[c + P + 1], wSW = w[c - P - 1], wNW = w[c + P - 1], wSE = w[c - P + 1];
-  const double sE = s[c + 1], sW = s[c - 1], sN = s[c + P], sS = s[c - P];
-  const double sNE = s[c + P + 1], sSW = s[c - P - 1], sNW = s[c + P - 1], sSE = s[c - P + 1];
-  const double j1 = k.gg * ((wE - wW) * (sN - sS) - (wN - wS) * (sE - sW));
-  const double j2 =
-      k.gg * (wE * (sNE - sSE) - wW * (sNW - sSW) - wN * (sNE - sNW) + wS * (sSE - sSW));
-  const double j3 =
-      k.gg * (wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS));
-  const double jac = (j1 + j2 + j3) * k.hh;
-  return -jac + (k.aa * (wE - 2.0 * wc + wW) + k.bb * (wN - 2.0 * wc + wS));
+  return cavity_rhs_vals(nine_at(w, c, P), nine_at(s, c, P), k);
+}
+
+template <int STAGE>
+__device__ __forceinline__ double cavity_update(double r, double w, double wn,
+                                                const CavCoef& k) {
+  if constexpr (STAGE == 0) return r;
+  else if constexpr (STAGE == 1) return w + k.dt * r;
+  else if constexpr (STAGE == 2) return (0.75 * wn + 0.25 * w) + k.c25dt * r;
+  else return (k.c13 * wn + k.c23 * w) + k.c23dt * r;
 }
 
 // Stage updates of lid_driven_cavity.jl:80, 89-93, 102-106 (interior only).
@@ -48,17 +73,142 @@ __global__ __launch_bounds__(kBX* kBY) void cavity_stage_kernel(
   if (i >= nx || j >= ny) return;
   const size_t c = (size_t)j * P + i;
   const double r = cavity_rhs_at(w, s, c, P, k);
-  double o;
-  if constexpr (STAGE == 0) {
-    o = r;
-  } else if constexpr (STAGE == 1) {
-    o = w[c] + k.dt * r;
-  } else if constexpr (STAGE == 2) {
-    o = (0.75 * wn[c] + 0.25 * w[c]) + k.c25dt * r;
-  } else {
-    o = (k.c13 * wn[c] + k.c23 * w[c]) + k.c23dt * r;
+  out[c] = cavity_update<STAGE>(r, w[c], STAGE >= 2 ? wn[c] : 0.0, k);
+}
+
+// Row-group variant of the stage kernel with the wall vorticity (bc2, below) fused in: a
+// 256-thread workgroup owns 512 consecutive i of 2 consecutive rows j0, j0 + 1 (j0 odd),
+// two i per lane loaded as 16 B from the 4 rows j0 - 1 .. j0 + 2 of omega and psi at once;
+// workgroups in row-major order, so the chip works on one narrow band of rows and each array
+// is one sequential stream.  i-neighbours by lane shuffles, across wavefronts through LDS,
+// the two halo columns of the workgroup by one load in the first wavefront.  Node i = 0 of
+// the first pair, row ny of the last group and anything outside the interior are loaded
+// (clamped) but not updated; instead the lanes and groups next to a wall write that wall's
+// omega from psi (lid_driven_cavity.jl:39-51; corners take the bottom / top formula, which
+// the reference applies last).  Needs nx a multiple of 512 and ny even.
+constexpr int kCavTileCols = 512;
+constexpr int kCavXcds = 8;
+
+struct W4 {
+  double l, a, b, r;
+};
+
+template <int STAGE>
+__global__ __launch_bounds__(256) void cavity_stage_tile_kernel(
+    const double* __restrict__ w, const double* __restrict__ s, const double* wn, double* out,
+    int nx, int ny, int P, CavCoef k, double dx2, double dy2, double dy) {
+  constexpr int G = 2, NR = G + 2, NW = 4, kWave = 64;
+  __shared__ double left[NW][2 * NR], right[NW][2 * NR];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int strips = nx / kCavTileCols, ngrp = ny / 2;
+  int strip = blockIdx.x % strips, grp = blockIdx.x / strips;
+  if (strips < kCavXcds && kCavXcds % strips == 0) {  // halo rows stay in one XCD's L2
+    const int bands = kCavXcds / strips;
+    if (ngrp % bands == 0) {
+      const int xcd = blockIdx.x % kCavXcds, i = blockIdx.x / kCavXcds;
+      strip = xcd % strips;
+      grp = (xcd / strips) * (ngrp / bands) + i;
+    }
   }
-  out[c] = o;
+  const int x0 = strip * kCavTileCols;
+  const int x = x0 + 2 * (int)threadIdx.x;  // <= nx - 2
+  const int j0 = 1 + grp * G;               // <= ny - 1
+
+  double2 wv[NR], sv[NR], wnv[G];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const size_t row = (size_t)min(j0 - 1 + j, ny) * P;
+    wv[j] = *reinterpret_cast<const double2*>(w + row + x);
+    sv[j] = *reinterpret_cast<const double2*>(s + row + x);
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    wnv[j] = make_double2(0.0, 0.0);
+    if constexpr (STAGE >= 2)
+      wnv[j] = *reinterpret_cast<const double2*>(wn + (size_t)min(j0 + j, ny) * P + x);
+  }
+  static_assert(4 * NR <= kWave, "halo fetch needs one lane per value");
+  double halo = 0.0;
+  if (threadIdx.x < 4 * NR) {
+    const int side = threadIdx.x / (2 * NR), rem = threadIdx.x % (2 * NR);
+    const int xh = side == 0 ? max(x0 - 1, 0) : x0 + kCavTileCols;  // <= nx
+    const size_t row = (size_t)min(j0 - 1 + rem / 2, ny) * P;
+    halo = ((rem & 1) ? s : w)[row + xh];
+  }
+  if ((lane == 0 && wave > 0) || (lane == kWave - 1 && wave < NW - 1)) {
+    double* e = lane == 0 ? right[wave - 1] : left[wave + 1];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      e[2 * j] = lane == 0 ? wv[j].x : wv[j].y;
+      e[2 * j + 1] = lane == 0 ? sv[j].x : sv[j].y;
+    }
+  }
+  if (threadIdx.x < 4 * NR) {
+    const int side = threadIdx.x / (2 * NR), rem = threadIdx.x % (2 * NR);
+    (side == 0 ? left[0] : right[NW - 1])[rem] = halo;
+  }
+  __syncthreads();
+  W4 ww[NR], sw[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    ww[j].a = wv[j].x;
+    ww[j].b = wv[j].y;
+    sw[j].a = sv[j].x;
+    sw[j].b = sv[j].y;
+    ww[j].l = __shfl_up(wv[j].y, 1, kWave);
+    ww[j].r = __shfl_down(wv[j].x, 1, kWave);
+    sw[j].l = __shfl_up(sv[j].y, 1, kWave);
+    sw[j].r = __shfl_down(sv[j].x, 1, kWave);
+    if (lane == 0) {
+      ww[j].l = left[wave][2 * j];
+      sw[j].l = left[wave][2 * j + 1];
+    }
+    if (lane == kWave - 1) {
+      ww[j].r = right[wave][2 * j];
+      sw[j].r = right[wave][2 * j + 1];
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const int jr = j0 + j;
+    if (jr >= ny) continue;  // row ny of the last group: a wall
+    const W4 &wm = ww[j], &wc = ww[j + 1], &wp = ww[j + 2];
+    const W4 &sm = sw[j], &sc = sw[j + 1], &sp = sw[j + 2];
+    Nine n0, n1, m0, m1;  // cells i = x and i = x + 1
+    n0.c = wc.a; n0.E = wc.b; n0.W = wc.l; n0.N = wp.a; n0.S = wm.a;
+    n0.NE = wp.b; n0.SW = wm.l; n0.NW = wp.l; n0.SE = wm.b;
+    n1.c = wc.b; n1.E = wc.r; n1.W = wc.a; n1.N = wp.b; n1.S = wm.b;
+    n1.NE = wp.r; n1.SW = wm.a; n1.NW = wp.a; n1.SE = wm.r;
+    m0.c = sc.a; m0.E = sc.b; m0.W = sc.l; m0.N = sp.a; m0.S = sm.a;
+    m0.NE = sp.b; m0.SW = sm.l; m0.NW = sp.l; m0.SE = sm.b;
+    m1.c = sc.b; m1.E = sc.r; m1.W = sc.a; m1.N = sp.b; m1.S = sm.b;
+    m1.NE = sp.r; m1.SW = sm.a; m1.NW = sp.a; m1.SE = sm.r;
+    double2 o;
+    o.x = cavity_update<STAGE>(cavity_rhs_vals(n0, m0, k), wc.a, wnv[j].x, k);
+    o.y = cavity_update<STAGE>(cavity_rhs_vals(n1, m1, k), wc.b, wnv[j].y, k);
+    double* orow = out + (size_t)jr * P;
+    if (x == 0) {  // node 0 is the left wall
+      o.x = (-4.0 * sc.b + 0.5 * sc.r) / dx2;
+    }
+    *reinterpret_cast<double2*>(orow + x) = o;
+    if (x == nx - 2) orow[nx] = (-4.0 * sc.b + 0.5 * sc.a) / dx2;  // right wall
+  }
+  if (j0 == 1) {  // bottom wall, row 0: psi rows 1 and 2 are sw[1], sw[2]
+    double2 o;
+    o.x = (-4.0 * sw[1].a + 0.5 * sw[2].a) / dy2;
+    o.y = (-4.0 * sw[1].b + 0.5 * sw[2].b) / dy2;
+    *reinterpret_cast<double2*>(out + x) = o;
+    if (x == nx - 2) out[nx] = (-4.0 * sw[1].r + 0.5 * sw[2].r) / dy2;
+  }
+  if (j0 == ny - 1) {  // top wall, row ny: psi rows ny - 1 and ny - 2 are sw[1], sw[0]
+    double* orow = out + (size_t)ny * P;
+    double2 o;
+    o.x = (-4.0 * sw[1].a + 0.5 * sw[0].a) / dy2 - 3.0 / dy;
+    o.y = (-4.0 * sw[1].b + 0.5 * sw[0].b) / dy2 - 3.0 / dy;
+    *reinterpret_cast<double2*>(orow + x) = o;
+    if (x == nx - 2) orow[nx] = (-4.0 * sw[1].r + 0.5 * sw[0].r) / dy2 - 3.0 / dy;
+  }
 }
 
 // lid_driven_cavity.jl:39-51: Jensen wall vorticity.  The reference's bottom/top loop runs
@@ -1009,6 +1159,30 @@ struct cfdj_cavity {
     CFDJ_HIP(hipGetLastError());
   }
 
+  // One RK stage on the interior plus the wall vorticity of the result, both from the same
+  // psi: one fused row-group kernel where the grid allows, else the two kernels.
+  // CFDJ_CAVITY_TILE=0 at handle creation keeps the two separate kernels (A/B, tests)
+  bool tile_ok = [] {
+    const char* e = std::getenv("CFDJ_CAVITY_TILE");
+    return !(e && e[0] == '0');
+  }();
+  void stage_bc(int st_, const double* w, double* out, double dt, const double* psi) {
+    if (tile_ok && st_ >= 1 && nx % kCavTileCols == 0 && ny % 2 == 0) {
+      const CavCoef k = coef(dt);
+      const dim3 g((unsigned)((nx / kCavTileCols) * (ny / 2))), b(256);
+      const double dx2 = dx * dx, dy2 = dy * dy;
+      switch (st_) {
+        case 1: hipLaunchKernelGGL(cavity_stage_tile_kernel<1>, g, b, 0, stream, w, psi, wn, out, nx, ny, P, k, dx2, dy2, dy); break;
+        case 2: hipLaunchKernelGGL(cavity_stage_tile_kernel<2>, g, b, 0, stream, w, psi, wn, out, nx, ny, P, k, dx2, dy2, dy); break;
+        default: hipLaunchKernelGGL(cavity_stage_tile_kernel<3>, g, b, 0, stream, w, psi, wn, out, nx, ny, P, k, dx2, dy2, dy); break;
+      }
+      CFDJ_HIP(hipGetLastError());
+      return;
+    }
+    stage(st_, w, out, dt, psi);
+    bc2(out, psi);
+  }
+
   void bc2(double* w) { bc2(w, sn); }
   void bc2(double* w, const double* sn) {
     hipLaunchKernelGGL(bc2_kernel, dim3((nx + ny + 255) / 256), dim3(256), 0, stream, w, sn,
@@ -1024,16 +1198,13 @@ struct cfdj_cavity {
       // leaves the per-workgroup sums of (psi_new - psi_old)^2
       double* A = sn;
       double* B = sp;
-      stage(1, wn, wa, dt, A);
-      bc2(wa, A);
+      stage_bc(1, wn, wa, dt, A);
       DstPoissonArgs a = dst_args(wa, B);
       for (int pass = 0; pass < 3; ++pass) launch_dst_poisson_pass(pass, a, stream);
-      stage(2, wa, wb, dt, B);
-      bc2(wb, B);
+      stage_bc(2, wa, wb, dt, B);
       a = dst_args(wb, B);
       for (int pass = 0; pass < 3; ++pass) launch_dst_poisson_pass(pass, a, stream);
-      stage(3, wb, wn, dt, B);
-      bc2(wn, B);
+      stage_bc(3, wb, wn, dt, B);
       a = dst_args(wn, B);
       a.sprev = A;
       a.part = part;
@@ -1046,14 +1217,11 @@ struct cfdj_cavity {
       return;
     }
     CFDJ_HIP(hipMemcpyAsync(sp, sn, field() * sizeof(double), hipMemcpyDeviceToDevice, stream));
-    stage(1, wn, wa, dt);  // wt = wn + dt r(wn, sn)
-    bc2(wa);
+    stage_bc(1, wn, wa, dt, sn);  // wt = wn + dt r(wn, sn)
     poisson_solve(wa, sn);
-    stage(2, wa, wb, dt);  // wt = (.75wn + .25wt) + .25dt r(wt, sn)
-    bc2(wb);
+    stage_bc(2, wa, wb, dt, sn);  // wt = (.75wn + .25wt) + .25dt r(wt, sn)
     poisson_solve(wb, sn);
-    stage(3, wb, wn, dt);  // wn = ((1/3)wn + (2/3)wt) + (2/3)dt r(wt, sn)
-    bc2(wn);
+    stage_bc(3, wb, wn, dt, sn);  // wn = ((1/3)wn + (2/3)wt) + (2/3)dt r(wt, sn)
     poisson_solve(wn, sn);
     launch_rms(sn, sp, 0, nx + 1, 0, ny + 1, P, (double)(nx + 1) * (ny + 1), part, kParts,
                d_rms + k, stream);
