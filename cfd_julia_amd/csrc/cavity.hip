@@ -393,7 +393,25 @@ __device__ __forceinline__ double mg_div(double x, double d) {
 //
 // Thread layout: 64 lanes along x (one lane per pair of nodes of a 128-node LDS row: the
 // lane's node of the half sweep's colour), 4 wavefronts taking every fourth row.
-template <int S, bool RCP>
+//
+// DESC (the descent's smoothing call): the halo is two nodes wider, so after the sweeps the
+// iterate is valid two nodes beyond the tile, the residual (Common.jl:239-246) one node
+// beyond it, and the tile's share of the next steps of the descent comes from LDS instead
+// of three more passes over the level: the sum of squares of the residual (the norm of
+// Common.jl:229-232, level 0), the residual itself where the one-workgroup coarse kernel
+// wants it in memory, and the full-weighting restriction to the next level (Common.jl:21-48;
+// its boundary nodes inject the residual's boundary, which is zero) with that level's
+// iterate zeroed (mg_N.jl:88) -- the same expressions in the same order as the separate
+// kernels.
+struct MgDescArgs {
+  double* rout;  // residual of this level, or nullptr
+  double* part;  // per-workgroup sums of r^2, or nullptr
+  double* fc;    // next level's right-hand side, or nullptr
+  double* ucz;   // next level's iterate (zeroed), with fc
+  int nxc, nyc, Pc;
+};
+
+template <int S, bool RCP, bool DESC>
 __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __restrict__ f,
                                                               const double* __restrict__ uin,
                                                               double* __restrict__ uout, int nx,
@@ -401,9 +419,10 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
                                                               double dy2, double dd,
                                                               const double* __restrict__ ucor,
                                                               int Pc,
-                                                              const int* __restrict__ ctl) {
+                                                              const int* __restrict__ ctl,
+                                                              const MgDescArgs da) {
   if (mg_done(ctl)) return;
-  constexpr int H = 2 * S, W = kFsW, TX = W - 2 * H, HT = kFsTY + 2 * H;
+  constexpr int H = 2 * S + (DESC ? 2 : 0), W = kFsW, TX = W - 2 * H, HT = kFsTY + 2 * H;
   __shared__ double su[HT * W];
   __shared__ double sf[HT * W];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
@@ -481,6 +500,69 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
       if (gi + 1 <= nx) *reinterpret_cast<double2*>(uout + (size_t)gj * P + gi) = v;
       else uout[(size_t)gj * P + gi] = v.x;
     }
+  if constexpr (DESC) {
+    // residual on the tile and one node around it, in place of f (zero off the interior)
+    constexpr int lo = 2 * S + 1;
+    for (int lj = lo + ty; lj <= HT - 1 - lo; lj += 4) {
+      const int gj = y0 + lj;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const int li = 2 * tx + e, gx = x0 + li;
+        if (li >= lo && li <= W - 1 - lo) {
+          const int c = lj * W + li;
+          double rc = 0.0;
+          if (gx >= 1 && gx < nx && gj >= 1 && gj < ny) {
+            const double uc = su[c];
+            rc = sf[c] - (mg_div<RCP>(su[c + 1] - 2.0 * uc + su[c - 1], dx2) +
+                          mg_div<RCP>(su[c + W] - 2.0 * uc + su[c - W], dy2));
+          }
+          sf[c] = rc;
+        }
+      }
+    }
+    __syncthreads();
+    double acc = 0.0;
+    if (2 * tx >= H && 2 * tx < H + TX && gi <= nx && (da.rout != nullptr || da.part != nullptr))
+      for (int lj = H + ty; lj < H + kFsTY; lj += 4) {
+        const int gj = y0 + lj;
+        if (gj > ny) break;
+        double2 v = *reinterpret_cast<const double2*>(sf + lj * W + 2 * tx);
+        if (gi + 1 > nx) v.y = 0.0;
+        acc += v.x * v.x + v.y * v.y;
+        if (da.rout != nullptr) {
+          if (gi + 1 <= nx) *reinterpret_cast<double2*>(da.rout + (size_t)gj * P + gi) = v;
+          else da.rout[(size_t)gj * P + gi] = v.x;
+        }
+      }
+    if (da.fc != nullptr) {
+      const int I0 = (x0 + H) >> 1, J0 = (y0 + H) >> 1;  // x0 + H, y0 + H are even
+      for (int e = threadIdx.x; e < (TX / 2) * (kFsTY / 2); e += 256) {
+        const int ci = e % (TX / 2), cj = e / (TX / 2);
+        const int I = I0 + ci, J = J0 + cj;
+        if (I > da.nxc || J > da.nyc) continue;
+        double v = 0.0;
+        if (I > 0 && I < da.nxc && J > 0 && J < da.nyc) {
+          const int c = (H + 2 * cj) * W + H + 2 * ci;
+          const double center = 4.0 * sf[c];
+          const double grid = 2.0 * (sf[c + W] + sf[c - W] + sf[c + 1] + sf[c - 1]);
+          const double corner = sf[c + W + 1] + sf[c - W + 1] + sf[c + W - 1] + sf[c - W - 1];
+          v = (center + grid + corner) / 16.0;
+        }
+        da.fc[(size_t)J * da.Pc + I] = v;
+        da.ucz[(size_t)J * da.Pc + I] = 0.0;
+      }
+    }
+    if (da.part != nullptr) {
+      __shared__ double red[256];
+      red[threadIdx.x] = acc;
+      __syncthreads();
+      for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+        __syncthreads();
+      }
+      if (threadIdx.x == 0) da.part[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
+    }
+  }
 }
 
 // Common.jl:239-246 residual; with part != nullptr also this block's sum of r^2 (fixed
@@ -741,7 +823,10 @@ struct Multigrid {
   std::vector<double*> alt;
   std::vector<char> fused_lvl, flip;
   double* part = nullptr;        // block partials of the level-0 residual norm
-  int nparts = 0;
+  int nparts = 0;                // ... of mg_residual_kernel's grid (= the buffer's size)
+  int nparts_cur = 0;            // ... written by the kernel that produced the current sums
+  bool fuse_desc = true;         // descent residual / norm / restriction inside the smoother
+  bool keep_r0 = false;          // level 0's residual is wanted in memory (cfdj_mg_residual)
   int* ctl = nullptr;            // device: [0] converged, [1] norms recorded, [2] spare
   double* hist = nullptr;        // device residual-norm history
   int hist_cap = 0;
@@ -794,6 +879,8 @@ struct Multigrid {
     alt.assign(nlev, nullptr);
     fused_lvl.assign(nlev, 0);
     flip.assign(nlev, 0);
+    const char* de = std::getenv("CFDJ_MG_FUSED_DESC");
+    fuse_desc = !(de && de[0] == '0');
     const char* fe = std::getenv("CFDJ_MG_FUSED_SMOOTH");
     const bool want = !(fe && fe[0] == '0');
     auto ok = [](int v) { return v >= 1 && v <= 3; };
@@ -869,17 +956,23 @@ struct Multigrid {
   }
   // `sweeps` red-black sweeps on level l; cor >= 0: first add the prolongation of level
   // cor's iterate (the ascent's correction step).
-  void smooth(int l, int sweeps, int cor = -1) {
+  void smooth(int l, int sweeps, int cor = -1) { smooth(l, sweeps, cor, nullptr); }
+  // desc != nullptr: the descent's call, with the residual / norm partials / restriction
+  // of the level fused in (fused levels only: see fuses()).
+  bool fuses(int l, int sweeps) const { return fused_lvl[l] && sweeps >= 1 && sweeps <= 3; }
+  void smooth(int l, int sweeps, int cor, const MgDescArgs* desc) {
     const double dx2 = ldx[l] * ldx[l], dy2 = ldy[l] * ldy[l];
     const double dd = -2.0 / dx2 - 2.0 / dy2;
-    const bool fuse = fused_lvl[l] && sweeps >= 1 && sweeps <= 3;
+    const bool fuse = fuses(l, sweeps);
+    if (desc && !fuse) throw Error{CFDJ_ERR_STATE, "multigrid: fused descent on an unfused level"};
     if (cor >= 0 && !fuse)
       hipLaunchKernelGGL(mg_prolong_add_kernel, interior_grid(lnx[l], lny[l]), dim3(kBX, kBY), 0,
                          st, ucur(cor), ucur(l), lnx[l], lny[l], lP[l], lP[cor], ctl);
     if (fuse) {
       const double* ucor = cor >= 0 ? ucur(cor) : nullptr;
       const int Pc = cor >= 0 ? lP[cor] : 0;
-      const int tx = kFsW - 4 * sweeps;  // tile width of mg_smooth_fused_kernel<sweeps>
+      // tile width of mg_smooth_fused_kernel<sweeps, ., desc>
+      const int tx = kFsW - 4 * sweeps - (desc ? 4 : 0);
       const dim3 g((lnx[l] + 1 + tx - 1) / tx, (lny[l] + 1 + kFsTY - 1) / kFsTY);
       const double* in = ucur(l);
       flip[l] ^= 1;
@@ -891,14 +984,31 @@ struct Multigrid {
       };
       const bool rcp = pow2(dx2) && pow2(dy2) && pow2(dd);
       const double a = rcp ? 1.0 / dx2 : dx2, b = rcp ? 1.0 / dy2 : dy2, c = rcp ? 1.0 / dd : dd;
-#define CFDJ_FS(S, R)                                                                           \
-  hipLaunchKernelGGL((mg_smooth_fused_kernel<S, R>), g, dim3(256), 0, st, f[l], in, out, lnx[l], \
-                     lny[l], lP[l], a, b, c, ucor, Pc, ctl)
-      switch (sweeps) {
-        case 1: if (rcp) CFDJ_FS(1, true); else CFDJ_FS(1, false); break;
-        case 2: if (rcp) CFDJ_FS(2, true); else CFDJ_FS(2, false); break;
-        default: if (rcp) CFDJ_FS(3, true); else CFDJ_FS(3, false); break;
+      const MgDescArgs da = desc ? *desc : MgDescArgs{};
+      if (desc && desc->part) {
+        if ((int)(g.x * g.y) > nparts)
+          throw Error{CFDJ_ERR_STATE, "multigrid: norm partial buffer too small"};
+        nparts_cur = (int)(g.x * g.y);
       }
+#define CFDJ_FS(S, R, D)                                                                   \
+  hipLaunchKernelGGL((mg_smooth_fused_kernel<S, R, D>), g, dim3(256), 0, st, f[l], in, out, \
+                     lnx[l], lny[l], lP[l], a, b, c, ucor, Pc, ctl, da)
+#define CFDJ_FS_S(S)                           \
+  do {                                         \
+    if (desc) {                                \
+      if (rcp) CFDJ_FS(S, true, true);         \
+      else CFDJ_FS(S, false, true);            \
+    } else {                                   \
+      if (rcp) CFDJ_FS(S, true, false);        \
+      else CFDJ_FS(S, false, false);           \
+    }                                          \
+  } while (0)
+      switch (sweeps) {
+        case 1: CFDJ_FS_S(1); break;
+        case 2: CFDJ_FS_S(2); break;
+        default: CFDJ_FS_S(3); break;
+      }
+#undef CFDJ_FS_S
 #undef CFDJ_FS
       return;
     }
@@ -908,34 +1018,59 @@ struct Multigrid {
         hipLaunchKernelGGL(mg_rbgs_kernel, g, dim3(kBX, kBY), 0, st, f[l], ucur(l), lnx[l],
                            lny[l], lP[l], dx2, dy2, dd, parity, ctl);
   }
-  void residual(int l, bool with_norm) {
+  void residual(int l, bool with_norm, bool always = false) {
     hipLaunchKernelGGL(mg_residual_kernel, interior_grid(lnx[l], lny[l]), dim3(kBX, kBY), 0, st,
                        f[l], ucur(l), r[l], lnx[l], lny[l], lP[l], ldx[l] * ldx[l],
-                       ldy[l] * ldy[l], with_norm ? part : nullptr, ctl);
+                       ldy[l] * ldy[l], with_norm ? part : nullptr, always ? nullptr : ctl);
+    if (with_norm) nparts_cur = nparts;
   }
   void norm0(double tol, bool first) {  // Common.jl:229-232 of level 0's residual
-    hipLaunchKernelGGL(mg_norm_kernel, dim3(1), dim3(1024), 0, st, part, nparts,
+    hipLaunchKernelGGL(mg_norm_kernel, dim3(1), dim3(1024), 0, st, part, nparts_cur,
                        (double)(lnx[0] - 1) * (lny[0] - 1), hist, hist_cap, ctl, tol,
                        first ? 1 : 0);
   }
+  void restrict_to(int k) {  // residual of level k - 1 -> f[k], u[k] = 0
+    hipLaunchKernelGGL(mg_restrict_kernel,
+                       dim3((lnx[k] + 1 + kBX - 1) / kBX, (lny[k] + 1 + kBY - 1) / kBY),
+                       dim3(kBX, kBY), 0, st, r[k - 1], f[k], ucur(k), lnx[k - 1], lny[k - 1],
+                       lP[k - 1], lnx[k], lny[k], lP[k], ctl);
+  }
 
-  // One iteration of the mg_N.jl:53-106 loop body.
+  // One iteration of the mg_N.jl:53-106 loop body.  Descent on the levels above the
+  // one-workgroup coarse kernel: smoothing, residual (level 0: its norm and the convergence
+  // test), restriction to the next level -- one kernel per level where the smoother is the
+  // fused one, else one kernel per step.
   void cycle(double tol) {
-    smooth(0, v1);
-    residual(0, true);
-    norm0(tol, false);
-    for (int k = 1; k < nlev && k < kc; ++k) {
-      if (k > 1) residual(k - 1, false);
-      hipLaunchKernelGGL(mg_restrict_kernel,
-                         dim3((lnx[k] + 1 + kBX - 1) / kBX, (lny[k] + 1 + kBY - 1) / kBY),
-                         dim3(kBX, kBY), 0, st, r[k - 1], f[k], ucur(k), lnx[k - 1], lny[k - 1],
-                         lP[k - 1], lnx[k], lny[k], lP[k], ctl);
-      smooth(k, k < nlev - 1 ? v1 : v2);
+    const int L = kc < nlev ? kc : nlev;  // levels 0..L-1 run as grid-wide kernels
+    for (int l = 0; l < L; ++l) {
+      const int sweeps = l < nlev - 1 ? v1 : v2;
+      const bool next = l + 1 < L;                   // restriction to a grid-wide level
+      const bool coarse = l == L - 1 && kc < nlev;   // residual read by the coarse kernel
+      if (fuse_desc && fuses(l, sweeps) && (next || coarse)) {
+        MgDescArgs da{};
+        da.part = l == 0 ? part : nullptr;
+        da.rout = coarse || (l == 0 && keep_r0) ? r[l] : nullptr;
+        if (next) {
+          da.fc = f[l + 1];
+          da.ucz = ucur(l + 1);
+          da.nxc = lnx[l + 1];
+          da.nyc = lny[l + 1];
+          da.Pc = lP[l + 1];
+        }
+        smooth(l, sweeps, -1, &da);
+        if (l == 0) norm0(tol, false);
+        continue;
+      }
+      smooth(l, sweeps);
+      if (l == 0) {
+        residual(0, true);
+        norm0(tol, false);
+      } else if (next || coarse) {
+        residual(l, false);
+      }
+      if (next) restrict_to(l + 1);
     }
-    if (kc < nlev) {
-      if (kc > 1) residual(kc - 1, false);
-      hipLaunchKernelGGL(mg_coarse_kernel, dim3(1), dim3(1024), coarse_lds, st, ca);
-    }
+    if (kc < nlev) hipLaunchKernelGGL(mg_coarse_kernel, dim3(1), dim3(1024), coarse_lds, st, ca);
     for (int k = (kc < nlev ? kc : nlev - 1); k >= 1; --k) smooth(k - 1, v3, k);
     CFDJ_HIP(hipGetLastError());
     for (int l = 0; l < nlev; ++l)
@@ -1448,6 +1583,7 @@ int cfdj_mg_create(int nx, int ny, double dx, double dy, int n_level, int v1, in
     CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
     h->nx = nx;
     h->ny = ny;
+    h->mg.keep_r0 = true;  // cfdj_mg_residual returns the residual mg_N.jl leaves in r
     h->mg.init(nx, ny, dx, dy, n_level, v1, v2, v3, h->stream);
     const size_t n = (size_t)(nx + 2) * (ny + 1);
     h->u = dalloc<double>(n);

@@ -213,8 +213,17 @@ __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
 }
 
 // One mode pair per workgroup: packed y-DST, times iden, packed y-DST, in place.
+#ifndef CFDJ_DST_COLS_WAVES
+#define CFDJ_DST_COLS_WAVES 3
+#endif
+// Wavefronts per SIMD the kernel is compiled for (the register cap): one per resident
+// 256-thread workgroup at M2 = 4096.
 template <int M2>
-__global__ __launch_bounds__(Plan<M2>::T) void dst_cols_kernel(double2* __restrict__ T, int JT,
+constexpr int dst_cols_waves() { return M2 <= 4096 ? CFDJ_DST_COLS_WAVES : 2; }
+
+template <int M2>
+__global__ __launch_bounds__(Plan<M2>::T)
+    __attribute__((amdgpu_waves_per_eu(dst_cols_waves<M2>(), dst_cols_waves<M2>()))) void dst_cols_kernel(double2* __restrict__ T, int JT,
                                                              const double* __restrict__ tx,
                                                              const double* __restrict__ ty,
                                                              double scale,
@@ -222,7 +231,7 @@ __global__ __launch_bounds__(Plan<M2>::T) void dst_cols_kernel(double2* __restri
   using PL = Plan<M2>;
   static_assert(PL::NSTAGES >= 2, "column length");
   constexpr int ny = M2 / 2;
-  __shared__ double2 lds[PL::PAD];
+  __shared__ double lds[PL::PAD];  // one component at a time (exchange_half): 3 per CU
   const TwGlobal<M2> tw{tw_};
   const int tid = threadIdx.x;
   const int kap = xcd_remap(blockIdx.x, gridDim.x);
@@ -242,9 +251,7 @@ __global__ __launch_bounds__(Plan<M2>::T) void dst_cols_kernel(double2* __restri
       a[b * R0 + r] = zero ? make_double2(0.0, 0.0) : make_double2(s * c.x, s * c.y);
     }
   stage_regs<M2, 0, -1>(a, tid, tw);
-  lds_write<M2, 0>(lds, a, tid);
-  __syncthreads();
-  run_stages<M2, 1, -1, false>(lds, a, tid, tw);  // last stage stays in registers
+  run_stages_half<M2, 1, -1>(lds, a, tid, tw);  // last stage stays in registers
 
   double2 v[16];
   fwd_to_inv<M2>(a, v);  // v[r] = Z[p], p = tid + T r
@@ -261,11 +268,8 @@ __global__ __launch_bounds__(Plan<M2>::T) void dst_cols_kernel(double2* __restri
     const double2 z = make_double2((-v[r].y * ia) * scale, (v[r].x * ib) * scale);
     v[r] = zero ? make_double2(0.0, 0.0) : z;
   }
-  __syncthreads();  // LDS is rewritten by the second transform's stage 0
   stage_regs<M2, 0, -1>(v, tid, tw);
-  lds_write<M2, 0>(lds, v, tid);
-  __syncthreads();
-  run_stages<M2, 1, -1, false>(lds, v, tid, tw);
+  run_stages_half<M2, 1, -1>(lds, v, tid, tw);
   constexpr int SL = PL::NSTAGES - 1;
   constexpr int RL = PL::radix(SL);
 #pragma unroll
