@@ -423,8 +423,11 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
                                                               const MgDescArgs da) {
   if (mg_done(ctl)) return;
   constexpr int H = 2 * S + (DESC ? 2 : 0), W = kFsW, TX = W - 2 * H, HT = kFsTY + 2 * H;
+  // Only u goes through LDS (neighbours belong to other lanes and wavefronts).  A lane
+  // updates nothing but its own two nodes (2 tx, 2 tx + 1) of its rows, so their f, their
+  // current u and, of the four neighbours, the lane's other node stay in registers.
   __shared__ double su[HT * W];
-  __shared__ double sf[HT * W];
+  __shared__ double sr[DESC ? HT * W : 1];  // the residual, for the restriction's stencil
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int x0 = blockIdx.x * TX - H, y0 = blockIdx.y * kFsTY - H;  // node of local (0, 0)
   // load: one 16-B access per lane covers a whole 128-node row (x0 and the pitch are even,
@@ -471,52 +474,77 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
       rf[k].y = 0.0;
     }
     *reinterpret_cast<double2*>(su + lj * W + 2 * tx) = ru[k];
-    *reinterpret_cast<double2*>(sf + lj * W + 2 * tx) = rf[k];
   }
   __syncthreads();
+  // f - lap(u) at the lane's node `odd` (local index c) of a row, from the registers (uc,
+  // the node's f, the lane's other node `own`: W if odd, else E) and three LDS reads
+  auto defect = [dx2, dy2](int odd, int c, double uc, double own, double fo) {
+    const double oth = su[odd ? c + 1 : c - 1];
+    const double uE = odd ? oth : own, uW = odd ? own : oth;
+    return fo - (mg_div<RCP>(uE - 2.0 * uc + uW, dx2) +
+                 mg_div<RCP>(su[c + W] - 2.0 * uc + su[c - W], dy2));
+  };
 #pragma unroll 1
   for (int h = 1; h <= 2 * S; ++h) {
     const int parity = (h - 1) & 1;
-    // valid region of this half sweep: local [h, W-1-h] x [h, HT-1-h]
-    for (int lj = h + ty; lj <= HT - 1 - h; lj += 4) {
+    // valid region of this half sweep: local [h, W-1-h] x [h, HT-1-h].  The nodes of one
+    // colour are independent of each other, so a lane's rows (every fourth) are unrolled
+    // and all their LDS reads are in flight together; the writes follow.
+    double res[ROWS];
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int lj = ty + 4 * k;
+      const int odd = (x0 + y0 + lj + parity) & 1;  // (node x + node y) % 2 == parity
+      const int li = 2 * tx + odd;
+      const int c = (lj >= 1 && lj <= HT - 2 ? lj : 1) * W + (li >= 1 && li <= W - 2 ? li : 1);
+      const double ux = ru[k].x, uy = ru[k].y, fx = rf[k].x, fy = rf[k].y;
+      const double uc = odd ? uy : ux;
+      const double own = odd ? ux : uy;
+      const double fo = odd ? fy : fx;
+      res[k] = uc + mg_div<RCP>(defect(odd, c, uc, own, fo), dd);
+    }
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int lj = ty + 4 * k;
       const int gj = y0 + lj;
-      const int li = 2 * tx + ((x0 + gj + parity) & 1);  // (node x + gj) % 2 == parity
+      const int odd = (x0 + gj + parity) & 1;
+      const int li = 2 * tx + odd;
       const int gx = x0 + li;
-      if (li >= h && li <= W - 1 - h && gx >= 1 && gx < nx && gj >= 1 && gj < ny) {
-        const int c = lj * W + li;
-        const double uc = su[c];
-        const double rt = sf[c] - (mg_div<RCP>(su[c + 1] - 2.0 * uc + su[c - 1], dx2) +
-                                   mg_div<RCP>(su[c + W] - 2.0 * uc + su[c - W], dy2));
-        su[c] = uc + mg_div<RCP>(rt, dd);
-      }
+      const bool act = lj >= h && lj <= HT - 1 - h && li >= h && li <= W - 1 - h && gx >= 1 &&
+                       gx < nx && gj >= 1 && gj < ny;
+      if (act) su[lj * W + li] = res[k];
+      // value selects, not a store through a selected address: the arrays stay in registers
+      ru[k].x = act && !odd ? res[k] : ru[k].x;
+      ru[k].y = act && odd ? res[k] : ru[k].y;
     }
     __syncthreads();
   }
-  if (2 * tx >= H && 2 * tx < H + TX && gi <= nx)
-    for (int lj = H + ty; lj < H + kFsTY; lj += 4) {
-      const int gj = y0 + lj;
-      if (gj > ny) break;
-      const double2 v = *reinterpret_cast<const double2*>(su + lj * W + 2 * tx);
-      if (gi + 1 <= nx) *reinterpret_cast<double2*>(uout + (size_t)gj * P + gi) = v;
-      else uout[(size_t)gj * P + gi] = v.x;
+  if (2 * tx >= H && 2 * tx < H + TX && gi <= nx) {
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int lj = ty + 4 * k, gj = y0 + lj;
+      if (lj >= H && lj < H + kFsTY && gj <= ny) {
+        if (gi + 1 <= nx) *reinterpret_cast<double2*>(uout + (size_t)gj * P + gi) = ru[k];
+        else uout[(size_t)gj * P + gi] = ru[k].x;
+      }
     }
+  }
   if constexpr (DESC) {
-    // residual on the tile and one node around it, in place of f (zero off the interior)
+    // residual on the tile and one node around it (zero off the interior)
     constexpr int lo = 2 * S + 1;
-    for (int lj = lo + ty; lj <= HT - 1 - lo; lj += 4) {
-      const int gj = y0 + lj;
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k) {
+      const int lj = ty + 4 * k, gj = y0 + lj;
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int li = 2 * tx + e, gx = x0 + li;
-        if (li >= lo && li <= W - 1 - lo) {
+        if (lj >= lo && lj <= HT - 1 - lo && li >= lo && li <= W - 1 - lo) {
           const int c = lj * W + li;
           double rc = 0.0;
-          if (gx >= 1 && gx < nx && gj >= 1 && gj < ny) {
-            const double uc = su[c];
-            rc = sf[c] - (mg_div<RCP>(su[c + 1] - 2.0 * uc + su[c - 1], dx2) +
-                          mg_div<RCP>(su[c + W] - 2.0 * uc + su[c - W], dy2));
-          }
-          sf[c] = rc;
+          if (gx >= 1 && gx < nx && gj >= 1 && gj < ny)
+            rc = defect(e, c, e ? ru[k].y : ru[k].x, e ? ru[k].x : ru[k].y,
+                        e ? rf[k].y : rf[k].x);
+          sr[c] = rc;
         }
       }
     }
@@ -526,7 +554,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
       for (int lj = H + ty; lj < H + kFsTY; lj += 4) {
         const int gj = y0 + lj;
         if (gj > ny) break;
-        double2 v = *reinterpret_cast<const double2*>(sf + lj * W + 2 * tx);
+        double2 v = *reinterpret_cast<const double2*>(sr + lj * W + 2 * tx);
         if (gi + 1 > nx) v.y = 0.0;
         acc += v.x * v.x + v.y * v.y;
         if (da.rout != nullptr) {
@@ -543,9 +571,9 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
         double v = 0.0;
         if (I > 0 && I < da.nxc && J > 0 && J < da.nyc) {
           const int c = (H + 2 * cj) * W + H + 2 * ci;
-          const double center = 4.0 * sf[c];
-          const double grid = 2.0 * (sf[c + W] + sf[c - W] + sf[c + 1] + sf[c - 1]);
-          const double corner = sf[c + W + 1] + sf[c - W + 1] + sf[c + W - 1] + sf[c - W - 1];
+          const double center = 4.0 * sr[c];
+          const double grid = 2.0 * (sr[c + W] + sr[c - W] + sr[c + 1] + sr[c - 1]);
+          const double corner = sr[c + W + 1] + sr[c - W + 1] + sr[c + W - 1] + sr[c - W - 1];
           v = (center + grid + corner) / 16.0;
         }
         da.fc[(size_t)J * da.Pc + I] = v;
