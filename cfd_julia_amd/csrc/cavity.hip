@@ -427,7 +427,6 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
   // updates nothing but its own two nodes (2 tx, 2 tx + 1) of its rows, so their f, their
   // current u and, of the four neighbours, the lane's other node stay in registers.
   __shared__ double su[HT * W];
-  __shared__ double sr[DESC ? HT * W : 1];  // the residual, for the restriction's stencil
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int x0 = blockIdx.x * TX - H, y0 = blockIdx.y * kFsTY - H;  // node of local (0, 0)
   // load: one 16-B access per lane covers a whole 128-node row (x0 and the pitch are even,
@@ -530,38 +529,47 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
     }
   }
   if constexpr (DESC) {
-    // residual on the tile and one node around it (zero off the interior)
+    // residual on the tile and one node around it (zero off the interior): into registers,
+    // then -- every lane done with u -- into the LDS buffer in place of u
     constexpr int lo = 2 * S + 1;
+    double2 rr[ROWS];
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
       const int lj = ty + 4 * k, gj = y0 + lj;
+      const int ljc = lj >= 1 && lj <= HT - 2 ? lj : 1;
+      double rc[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
         const int li = 2 * tx + e, gx = x0 + li;
-        if (lj >= lo && lj <= HT - 1 - lo && li >= lo && li <= W - 1 - lo) {
-          const int c = lj * W + li;
-          double rc = 0.0;
-          if (gx >= 1 && gx < nx && gj >= 1 && gj < ny)
-            rc = defect(e, c, e ? ru[k].y : ru[k].x, e ? ru[k].x : ru[k].y,
-                        e ? rf[k].y : rf[k].x);
-          sr[c] = rc;
+        const int c = ljc * W + (li >= 1 && li <= W - 2 ? li : 1);
+        const double d = defect(e, c, e ? ru[k].y : ru[k].x, e ? ru[k].x : ru[k].y,
+                                e ? rf[k].y : rf[k].x);
+        rc[e] = lj >= lo && lj <= HT - 1 - lo && li >= lo && li <= W - 1 - lo && gx >= 1 &&
+                        gx < nx && gj >= 1 && gj < ny
+                    ? d
+                    : 0.0;
+      }
+      rr[k] = make_double2(rc[0], rc[1]);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < ROWS; ++k)
+      *reinterpret_cast<double2*>(su + (ty + 4 * k) * W + 2 * tx) = rr[k];
+    __syncthreads();
+    double acc = 0.0;
+    if (2 * tx >= H && 2 * tx < H + TX && gi <= nx && (da.rout != nullptr || da.part != nullptr)) {
+#pragma unroll
+      for (int k = 0; k < ROWS; ++k) {
+        const int lj = ty + 4 * k, gj = y0 + lj;
+        if (lj >= H && lj < H + kFsTY && gj <= ny) {
+          acc += rr[k].x * rr[k].x + rr[k].y * rr[k].y;
+          if (da.rout != nullptr) {
+            if (gi + 1 <= nx) *reinterpret_cast<double2*>(da.rout + (size_t)gj * P + gi) = rr[k];
+            else da.rout[(size_t)gj * P + gi] = rr[k].x;
+          }
         }
       }
     }
-    __syncthreads();
-    double acc = 0.0;
-    if (2 * tx >= H && 2 * tx < H + TX && gi <= nx && (da.rout != nullptr || da.part != nullptr))
-      for (int lj = H + ty; lj < H + kFsTY; lj += 4) {
-        const int gj = y0 + lj;
-        if (gj > ny) break;
-        double2 v = *reinterpret_cast<const double2*>(sr + lj * W + 2 * tx);
-        if (gi + 1 > nx) v.y = 0.0;
-        acc += v.x * v.x + v.y * v.y;
-        if (da.rout != nullptr) {
-          if (gi + 1 <= nx) *reinterpret_cast<double2*>(da.rout + (size_t)gj * P + gi) = v;
-          else da.rout[(size_t)gj * P + gi] = v.x;
-        }
-      }
     if (da.fc != nullptr) {
       const int I0 = (x0 + H) >> 1, J0 = (y0 + H) >> 1;  // x0 + H, y0 + H are even
       for (int e = threadIdx.x; e < (TX / 2) * (kFsTY / 2); e += 256) {
@@ -571,9 +579,9 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
         double v = 0.0;
         if (I > 0 && I < da.nxc && J > 0 && J < da.nyc) {
           const int c = (H + 2 * cj) * W + H + 2 * ci;
-          const double center = 4.0 * sr[c];
-          const double grid = 2.0 * (sr[c + W] + sr[c - W] + sr[c + 1] + sr[c - 1]);
-          const double corner = sr[c + W + 1] + sr[c - W + 1] + sr[c + W - 1] + sr[c - W - 1];
+          const double center = 4.0 * su[c];
+          const double grid = 2.0 * (su[c + W] + su[c - W] + su[c + 1] + su[c - 1]);
+          const double corner = su[c + W + 1] + su[c - W + 1] + su[c + W - 1] + su[c - W - 1];
           v = (center + grid + corner) / 16.0;
         }
         da.fc[(size_t)J * da.Pc + I] = v;
