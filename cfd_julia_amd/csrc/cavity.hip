@@ -382,6 +382,10 @@ __global__ __launch_bounds__(kBX* kBY) void mg_rbgs_kernel(const double* __restr
 // reciprocals passed in their place -- the same bits, a third of the instructions (with the
 // data in LDS the kernel is bound by that arithmetic, not by memory).
 constexpr int kFsW = 128, kFsTY = 24;  // LDS row of 128 nodes: tile = (128 - 4S) x 24 nodes
+// wavefronts per tile on the small levels: the most (up to 16) that divide the tile's rows
+constexpr int fs_wide_nw(int ht) {
+  return ht % 16 == 0 ? 16 : ht % 14 == 0 ? 14 : ht % 12 == 0 ? 12 : ht % 10 == 0 ? 10 : 4;
+}
 template <bool RCP>
 __device__ __forceinline__ double mg_div(double x, double d) {
   return RCP ? x * d : x / d;
@@ -392,7 +396,10 @@ __device__ __forceinline__ double mg_div(double x, double d) {
 // separate pass over u before the smoothing.
 //
 // Thread layout: 64 lanes along x (one lane per pair of nodes of a 128-node LDS row: the
-// lane's node of the half sweep's colour), 4 wavefronts taking every fourth row.
+// lane's node of the half sweep's colour), NW wavefronts taking every NW-th row.  NW = 4
+// where the level has tiles enough to fill the chip several times over; on the small
+// levels, whose cost is the latency of one tile, 16 (12 for the descent's 36-row tile)
+// wavefronts share the tile's rows.
 //
 // DESC (the descent's smoothing call): the halo is two nodes wider, so after the sweeps the
 // iterate is valid two nodes beyond the tile, the residual (Common.jl:239-246) one node
@@ -411,8 +418,8 @@ struct MgDescArgs {
   int nxc, nyc, Pc;
 };
 
-template <int S, bool RCP, bool DESC>
-__global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __restrict__ f,
+template <int S, bool RCP, bool DESC, int NW>
+__global__ __launch_bounds__(64 * NW) void mg_smooth_fused_kernel(const double* __restrict__ f,
                                                               const double* __restrict__ uin,
                                                               double* __restrict__ uout, int nx,
                                                               int ny, int P, double dx2,
@@ -432,14 +439,14 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
   // load: one 16-B access per lane covers a whole 128-node row (x0 and the pitch are even,
   // so the pair (gi, gi + 1) is aligned; gi + 1 = nx + 1 is the arrays' padding column);
   // all of a wavefront's rows are requested before the first one is used
-  constexpr int ROWS = HT / 4;
-  static_assert(HT % 4 == 0, "rows per wavefront");
+  constexpr int ROWS = HT / NW, NT = 64 * NW;
+  static_assert(HT % NW == 0, "rows per wavefront");
   const int gi = x0 + 2 * tx;
   const bool xin = gi >= 0 && gi <= nx;
   double2 ru[ROWS], rf[ROWS];
 #pragma unroll
   for (int k = 0; k < ROWS; ++k) {
-    const int gj = y0 + ty + 4 * k;
+    const int gj = y0 + ty + NW * k;
     ru[k] = make_double2(0.0, 0.0);
     rf[k] = make_double2(0.0, 0.0);
     if (xin && gj >= 0 && gj <= ny) {
@@ -450,7 +457,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
   }
 #pragma unroll
   for (int k = 0; k < ROWS; ++k) {
-    const int lj = ty + 4 * k, gj = y0 + lj;
+    const int lj = ty + NW * k, gj = y0 + lj;
     if (ucor != nullptr && gj >= 1 && gj < ny) {
       const size_t qr = (size_t)(gj >> 1) * Pc;
 #pragma unroll
@@ -492,7 +499,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
     double res[ROWS];
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
-      const int lj = ty + 4 * k;
+      const int lj = ty + NW * k;
       const int odd = (x0 + y0 + lj + parity) & 1;  // (node x + node y) % 2 == parity
       const int li = 2 * tx + odd;
       const int c = (lj >= 1 && lj <= HT - 2 ? lj : 1) * W + (li >= 1 && li <= W - 2 ? li : 1);
@@ -504,7 +511,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
     }
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
-      const int lj = ty + 4 * k;
+      const int lj = ty + NW * k;
       const int gj = y0 + lj;
       const int odd = (x0 + gj + parity) & 1;
       const int li = 2 * tx + odd;
@@ -521,7 +528,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
   if (2 * tx >= H && 2 * tx < H + TX && gi <= nx) {
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
-      const int lj = ty + 4 * k, gj = y0 + lj;
+      const int lj = ty + NW * k, gj = y0 + lj;
       if (lj >= H && lj < H + kFsTY && gj <= ny) {
         if (gi + 1 <= nx) *reinterpret_cast<double2*>(uout + (size_t)gj * P + gi) = ru[k];
         else uout[(size_t)gj * P + gi] = ru[k].x;
@@ -535,7 +542,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
     double2 rr[ROWS];
 #pragma unroll
     for (int k = 0; k < ROWS; ++k) {
-      const int lj = ty + 4 * k, gj = y0 + lj;
+      const int lj = ty + NW * k, gj = y0 + lj;
       const int ljc = lj >= 1 && lj <= HT - 2 ? lj : 1;
       double rc[2];
 #pragma unroll
@@ -554,13 +561,13 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < ROWS; ++k)
-      *reinterpret_cast<double2*>(su + (ty + 4 * k) * W + 2 * tx) = rr[k];
+      *reinterpret_cast<double2*>(su + (ty + NW * k) * W + 2 * tx) = rr[k];
     __syncthreads();
     double acc = 0.0;
     if (2 * tx >= H && 2 * tx < H + TX && gi <= nx && (da.rout != nullptr || da.part != nullptr)) {
 #pragma unroll
       for (int k = 0; k < ROWS; ++k) {
-        const int lj = ty + 4 * k, gj = y0 + lj;
+        const int lj = ty + NW * k, gj = y0 + lj;
         if (lj >= H && lj < H + kFsTY && gj <= ny) {
           acc += rr[k].x * rr[k].x + rr[k].y * rr[k].y;
           if (da.rout != nullptr) {
@@ -572,7 +579,7 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
     }
     if (da.fc != nullptr) {
       const int I0 = (x0 + H) >> 1, J0 = (y0 + H) >> 1;  // x0 + H, y0 + H are even
-      for (int e = threadIdx.x; e < (TX / 2) * (kFsTY / 2); e += 256) {
+      for (int e = threadIdx.x; e < (TX / 2) * (kFsTY / 2); e += NT) {
         const int ci = e % (TX / 2), cj = e / (TX / 2);
         const int I = I0 + ci, J = J0 + cj;
         if (I > da.nxc || J > da.nyc) continue;
@@ -589,11 +596,11 @@ __global__ __launch_bounds__(256) void mg_smooth_fused_kernel(const double* __re
       }
     }
     if (da.part != nullptr) {
-      __shared__ double red[256];
-      red[threadIdx.x] = acc;
+      __shared__ double red[1024];  // fixed summation tree, whatever NT
+      for (int i = threadIdx.x; i < 1024; i += NT) red[i] = i < NT ? acc : 0.0;
       __syncthreads();
-      for (int off = 128; off > 0; off >>= 1) {
-        if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      for (int off = 512; off > 0; off >>= 1) {
+        for (int i = threadIdx.x; i < off; i += NT) red[i] += red[i + off];
         __syncthreads();
       }
       if (threadIdx.x == 0) da.part[blockIdx.y * gridDim.x + blockIdx.x] = red[0];
@@ -861,6 +868,7 @@ struct Multigrid {
   double* part = nullptr;        // block partials of the level-0 residual norm
   int nparts = 0;                // ... of mg_residual_kernel's grid (= the buffer's size)
   int nparts_cur = 0;            // ... written by the kernel that produced the current sums
+  int mg_cus = 256;              // compute units (tile-shape heuristic only)
   bool fuse_desc = true;         // descent residual / norm / restriction inside the smoother
   bool keep_r0 = false;          // level 0's residual is wanted in memory (cfdj_mg_residual)
   int* ctl = nullptr;            // device: [0] converged, [1] norms recorded, [2] spare
@@ -1026,24 +1034,33 @@ struct Multigrid {
           throw Error{CFDJ_ERR_STATE, "multigrid: norm partial buffer too small"};
         nparts_cur = (int)(g.x * g.y);
       }
-#define CFDJ_FS(S, R, D)                                                                   \
-  hipLaunchKernelGGL((mg_smooth_fused_kernel<S, R, D>), g, dim3(256), 0, st, f[l], in, out, \
-                     lnx[l], lny[l], lP[l], a, b, c, ucor, Pc, ctl, da)
-#define CFDJ_FS_S(S)                           \
-  do {                                         \
-    if (desc) {                                \
-      if (rcp) CFDJ_FS(S, true, true);         \
-      else CFDJ_FS(S, false, true);            \
-    } else {                                   \
-      if (rcp) CFDJ_FS(S, true, false);        \
-      else CFDJ_FS(S, false, false);           \
-    }                                          \
+      // wavefronts per tile: 4 when the level has several tiles per CU slot, else as many
+      // as divide the tile's rows (fs_wide_nw)
+      const bool wide = (long)g.x * g.y < 2L * mg_cus;
+#define CFDJ_FS(S, R, D, NW)                                                                \
+  hipLaunchKernelGGL((mg_smooth_fused_kernel<S, R, D, NW>), g, dim3(64 * NW), 0, st, f[l], in, \
+                     out, lnx[l], lny[l], lP[l], a, b, c, ucor, Pc, ctl, da)
+#define CFDJ_FS_R(S, R)                                                       \
+  do {                                                                        \
+    if (desc) {                                                               \
+      if (wide) CFDJ_FS(S, R, true, (fs_wide_nw(kFsTY + 4 * S + 4)));         \
+      else CFDJ_FS(S, R, true, 4);                                            \
+    } else {                                                                  \
+      if (wide) CFDJ_FS(S, R, false, (fs_wide_nw(kFsTY + 4 * S)));            \
+      else CFDJ_FS(S, R, false, 4);                                           \
+    }                                                                         \
+  } while (0)
+#define CFDJ_FS_S(S)            \
+  do {                          \
+    if (rcp) CFDJ_FS_R(S, true); \
+    else CFDJ_FS_R(S, false);   \
   } while (0)
       switch (sweeps) {
         case 1: CFDJ_FS_S(1); break;
         case 2: CFDJ_FS_S(2); break;
         default: CFDJ_FS_S(3); break;
       }
+#undef CFDJ_FS_R
 #undef CFDJ_FS_S
 #undef CFDJ_FS
       return;
