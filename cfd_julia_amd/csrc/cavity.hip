@@ -396,10 +396,8 @@ __device__ __forceinline__ double mg_div(double x, double d) {
 // separate pass over u before the smoothing.
 //
 // Thread layout: 64 lanes along x (one lane per pair of nodes of a 128-node LDS row: the
-// lane's node of the half sweep's colour), NW wavefronts taking every NW-th row.  NW = 4
-// where the level has tiles enough to fill the chip several times over; on the small
-// levels, whose cost is the latency of one tile, 16 (12 for the descent's 36-row tile)
-// wavefronts share the tile's rows.
+// lane's node of the half sweep's colour), NW wavefronts taking every NW-th row: 16 (12
+// for the descent's 36-row tile at S = 2), or 4 with 8-9 rows per lane.
 //
 // DESC (the descent's smoothing call): the halo is two nodes wider, so after the sweeps the
 // iterate is valid two nodes beyond the tile, the residual (Common.jl:239-246) one node
@@ -868,7 +866,6 @@ struct Multigrid {
   double* part = nullptr;        // block partials of the level-0 residual norm
   int nparts = 0;                // ... of mg_residual_kernel's grid (= the buffer's size)
   int nparts_cur = 0;            // ... written by the kernel that produced the current sums
-  int mg_cus = 256;              // compute units (tile-shape heuristic only)
   bool fuse_desc = true;         // descent residual / norm / restriction inside the smoother
   bool keep_r0 = false;          // level 0's residual is wanted in memory (cfdj_mg_residual)
   int* ctl = nullptr;            // device: [0] converged, [1] norms recorded, [2] spare
@@ -1034,9 +1031,14 @@ struct Multigrid {
           throw Error{CFDJ_ERR_STATE, "multigrid: norm partial buffer too small"};
         nparts_cur = (int)(g.x * g.y);
       }
-      // wavefronts per tile: 4 when the level has several tiles per CU slot, else as many
-      // as divide the tile's rows (fs_wide_nw)
-      const bool wide = (long)g.x * g.y < 2L * mg_cus;
+      // wavefronts per tile: as many as divide the tile's rows (fs_wide_nw) -- measured
+      // faster on every level of the 2048^2 cavity (small levels: the kernel's cost is one
+      // tile's latency; large ones: more rows in flight per CU) than 4 wavefronts taking
+      // 8-9 rows each, which CFDJ_MG_WIDE_TILES=0 restores
+      static const bool wide = [] {
+        const char* e = std::getenv("CFDJ_MG_WIDE_TILES");
+        return !(e && e[0] == '0');
+      }();
 #define CFDJ_FS(S, R, D, NW)                                                                \
   hipLaunchKernelGGL((mg_smooth_fused_kernel<S, R, D, NW>), g, dim3(64 * NW), 0, st, f[l], in, \
                      out, lnx[l], lny[l], lP[l], a, b, c, ucor, Pc, ctl, da)

@@ -192,9 +192,11 @@ def test_gpu_mg_fused_kernels_are_bit_identical(lib, monkeypatch, n, levels, swe
     from cfd_julia_amd import mg
 
     v1, v2, v3 = sweeps
-    keys = ("CFDJ_MG_FUSED_SMOOTH", "CFDJ_MG_FUSED_DESC", "CFDJ_MG_COARSE", "CFDJ_MG_GRAPH")
+    keys = ("CFDJ_MG_FUSED_SMOOTH", "CFDJ_MG_FUSED_DESC", "CFDJ_MG_COARSE", "CFDJ_MG_GRAPH",
+            "CFDJ_MG_WIDE_TILES")
     out = {}
     for name, env in (("fused", {}),
+                      ("narrow", {"CFDJ_MG_WIDE_TILES": "0"}),
                       ("nodesc", {"CFDJ_MG_FUSED_DESC": "0"}),
                       ("plain", {"CFDJ_MG_FUSED_SMOOTH": "0", "CFDJ_MG_COARSE": "0",
                                  "CFDJ_MG_GRAPH": "0"})):
@@ -207,9 +209,10 @@ def test_gpu_mg_fused_kernels_are_bit_identical(lib, monkeypatch, n, levels, swe
         it, hist = mg.mg_N(dx, dy, n, n, r, f, un, v1, v2, v3, 100000, 1e-9, n_level=levels)
         out[name] = (it, hist, un, r)
     assert out["plain"][0] > 2
-    for name in ("fused", "nodesc"):
+    for name in ("fused", "narrow", "nodesc"):
         assert out[name][0] == out["plain"][0], name
         assert np.array_equal(out[name][2], out["plain"][2]), name
         assert np.array_equal(out[name][3], out["plain"][3]), name
     assert np.array_equal(out["nodesc"][1], out["plain"][1])
     np.testing.assert_allclose(out["fused"][1], out["plain"][1], rtol=1e-13)
+    np.testing.assert_allclose(out["narrow"][1], out["plain"][1], rtol=1e-13)
