@@ -739,21 +739,27 @@ struct MgCoarseArgs {
   const int* ctl;
 };
 
+// Loops over a w-wide index range run over the next power of two and skip the excess, so
+// the (row, column) split is a shift and a mask instead of an integer division.
+__device__ __forceinline__ int ceil_log2(int w) { return w <= 1 ? 0 : 32 - __clz(w - 1); }
+
+template <bool RCP>
 __device__ __forceinline__ void lds_smooth(const double* f, double* u, int nx, int ny, int P,
                                            double dx2, double dy2, double dd, int sweeps) {
   const int hw = (nx + 1) / 2;
-  const int total = (ny - 1) * hw;
+  const int sh = ceil_log2(hw), mask = (1 << sh) - 1;
+  const int total = (ny - 1) << sh;
   for (int s = 0; s < sweeps; ++s)
     for (int parity = 0; parity < 2; ++parity) {
       for (int e = threadIdx.x; e < total; e += blockDim.x) {
-        const int j = 1 + e / hw;
-        const int i = 1 + 2 * (e % hw) + ((j + 1 + parity) & 1);
-        if (i < nx) {
+        const int j = 1 + (e >> sh);
+        const int i = 1 + 2 * (e & mask) + ((j + 1 + parity) & 1);
+        if ((e & mask) < hw && i < nx) {
           const int c = j * P + i;
           const double uc = u[c];
-          const double rt = f[c] - ((u[c + 1] - 2.0 * uc + u[c - 1]) / dx2 +
-                                    (u[c + P] - 2.0 * uc + u[c - P]) / dy2);
-          u[c] = uc + rt / dd;
+          const double rt = f[c] - (mg_div<RCP>(u[c + 1] - 2.0 * uc + u[c - 1], dx2) +
+                                    mg_div<RCP>(u[c + P] - 2.0 * uc + u[c - P], dy2));
+          u[c] = uc + mg_div<RCP>(rt, dd);
         }
       }
       __syncthreads();
@@ -763,9 +769,11 @@ __device__ __forceinline__ void lds_smooth(const double* f, double* u, int nx, i
 // restriction of a fine residual (any memory) into LDS f, u = 0
 __device__ __forceinline__ void lds_restrict(const double* r, int nxf, int nyf, int Pf, double* ec,
                                              double* uc, int nxc, int nyc, int Pc) {
-  const int total = (nxc + 1) * (nyc + 1);
+  const int sh = ceil_log2(nxc + 1), mask = (1 << sh) - 1;
+  const int total = (nyc + 1) << sh;
   for (int e = threadIdx.x; e < total; e += blockDim.x) {
-    const int j = e / (nxc + 1), i = e % (nxc + 1);
+    const int j = e >> sh, i = e & mask;
+    if (i > nxc) continue;
     double v;
     if (i == 0 || i == nxc || j == 0 || j == nyc) {
       v = r[(size_t)(j == 0 ? 0 : (j == nyc ? nyf : 2 * j)) * Pf +
@@ -783,6 +791,9 @@ __device__ __forceinline__ void lds_restrict(const double* r, int nxf, int nyf, 
   __syncthreads();
 }
 
+// RCP: every level's dx^2, dy^2 and diagonal are powers of two and the arguments hold their
+// reciprocals (exact): multiplications instead of divisions, the same bits.
+template <bool RCP>
 __global__ __launch_bounds__(1024) void mg_coarse_kernel(const MgCoarseArgs a) {
   if (mg_done(a.ctl)) return;
   extern __shared__ double sm[];
@@ -790,37 +801,40 @@ __global__ __launch_bounds__(1024) void mg_coarse_kernel(const MgCoarseArgs a) {
   // descent
   lds_restrict(a.r_in, a.nxf, a.nyf, a.Pf, sm + a.off_f[0], sm + a.off_u[0], a.lnx[0], a.lny[0],
                a.lP[0]);
-  lds_smooth(sm + a.off_f[0], sm + a.off_u[0], a.lnx[0], a.lny[0], a.lP[0], a.dx2[0], a.dy2[0],
-             a.dd[0], a.sweeps_down[0]);
+  lds_smooth<RCP>(sm + a.off_f[0], sm + a.off_u[0], a.lnx[0], a.lny[0], a.lP[0], a.dx2[0],
+                  a.dy2[0], a.dd[0], a.sweeps_down[0]);
   for (int c = 1; c < a.n; ++c) {
     // residual of level c-1 (Common.jl:239-246), boundary entries zero
     const int nx = a.lnx[c - 1], ny = a.lny[c - 1], P = a.lP[c - 1];
     const double* f = sm + a.off_f[c - 1];
     const double* u = sm + a.off_u[c - 1];
-    for (int e = threadIdx.x; e < (nx + 1) * (ny + 1); e += blockDim.x) {
-      const int j = e / (nx + 1), i = e % (nx + 1);
+    const int sh = ceil_log2(nx + 1), mask = (1 << sh) - 1;
+    for (int e = threadIdx.x; e < ((ny + 1) << sh); e += blockDim.x) {
+      const int j = e >> sh, i = e & mask;
+      if (i > nx) continue;
       double rc = 0.0;
       if (i >= 1 && i < nx && j >= 1 && j < ny) {
         const int q = j * P + i;
         const double uc = u[q];
-        rc = f[q] - ((u[q + 1] - 2.0 * uc + u[q - 1]) / a.dx2[c - 1] +
-                     (u[q + P] - 2.0 * uc + u[q - P]) / a.dy2[c - 1]);
+        rc = f[q] - (mg_div<RCP>(u[q + 1] - 2.0 * uc + u[q - 1], a.dx2[c - 1]) +
+                     mg_div<RCP>(u[q + P] - 2.0 * uc + u[q - P], a.dy2[c - 1]));
       }
       rb[j * P + i] = rc;
     }
     __syncthreads();
     lds_restrict(rb, nx, ny, P, sm + a.off_f[c], sm + a.off_u[c], a.lnx[c], a.lny[c], a.lP[c]);
-    lds_smooth(sm + a.off_f[c], sm + a.off_u[c], a.lnx[c], a.lny[c], a.lP[c], a.dx2[c], a.dy2[c],
-               a.dd[c], a.sweeps_down[c]);
+    lds_smooth<RCP>(sm + a.off_f[c], sm + a.off_u[c], a.lnx[c], a.lny[c], a.lP[c], a.dx2[c],
+                    a.dy2[c], a.dd[c], a.sweeps_down[c]);
   }
   // ascent
   for (int c = a.n - 1; c >= 1; --c) {
     const int nxf = a.lnx[c - 1], nyf = a.lny[c - 1], Pf = a.lP[c - 1], Pc = a.lP[c];
     const double* uc = sm + a.off_u[c];
     double* uf = sm + a.off_u[c - 1];
-    const int wdt = nxf - 1;
-    for (int e = threadIdx.x; e < wdt * (nyf - 1); e += blockDim.x) {
-      const int J = 1 + e / wdt, I = 1 + e % wdt;
+    const int sh = ceil_log2(nxf - 1), mask = (1 << sh) - 1;
+    for (int e = threadIdx.x; e < ((nyf - 1) << sh); e += blockDim.x) {
+      const int J = 1 + (e >> sh), I = 1 + (e & mask);
+      if (I >= nxf) continue;
       const int q = (J >> 1) * Pc + (I >> 1);
       double p;
       if (!(I & 1) && !(J & 1)) p = uc[q];
@@ -830,8 +844,8 @@ __global__ __launch_bounds__(1024) void mg_coarse_kernel(const MgCoarseArgs a) {
       uf[J * Pf + I] += p;
     }
     __syncthreads();
-    lds_smooth(sm + a.off_f[c - 1], uf, nxf, nyf, Pf, a.dx2[c - 1], a.dy2[c - 1], a.dd[c - 1],
-               a.v3);
+    lds_smooth<RCP>(sm + a.off_f[c - 1], uf, nxf, nyf, Pf, a.dx2[c - 1], a.dy2[c - 1],
+                    a.dd[c - 1], a.v3);
   }
   const double* u0 = sm + a.off_u[0];
   for (int e = threadIdx.x; e < a.lP[0] * (a.lny[0] + 1); e += blockDim.x) a.u_out[e] = u0[e];
@@ -873,6 +887,12 @@ struct Multigrid {
   int hist_cap = 0;
   int kc = 0;                    // first level held in LDS by mg_coarse_kernel (nlev: none)
   MgCoarseArgs ca;
+  bool ca_rcp = false;           // ca's dx2, dy2, dd hold exact reciprocals (powers of two)
+  static bool exact_pow2(double d) {
+    int e = 0;
+    const double m = std::frexp(std::fabs(d), &e);
+    return m == 0.5 && e > -500 && e < 500;
+  }
   size_t coarse_lds = 0;
   bool use_graph = true;
   hipGraphExec_t gexec = nullptr;
@@ -950,6 +970,7 @@ struct Multigrid {
     if (first >= nlev || nlev - first > kMgCoarseMaxLevels) return;
     size_t off = 0;
     ca = MgCoarseArgs();
+    ca_rcp = true;
     ca.n = nlev - first;
     for (int c = 0; c < ca.n; ++c) {
       const int l = first + c;
@@ -959,6 +980,7 @@ struct Multigrid {
       ca.dx2[c] = ldx[l] * ldx[l];
       ca.dy2[c] = ldy[l] * ldy[l];
       ca.dd[c] = -2.0 / ca.dx2[c] - 2.0 / ca.dy2[c];
+      ca_rcp = ca_rcp && exact_pow2(ca.dx2[c]) && exact_pow2(ca.dy2[c]) && exact_pow2(ca.dd[c]);
       ca.sweeps_down[c] = l < nlev - 1 ? v1 : v2;
       const size_t n = (size_t)lP[l] * (lny[l] + 1);
       ca.off_u[c] = (int)off;
@@ -977,8 +999,16 @@ struct Multigrid {
     ca.Pf = lP[first - 1];
     ca.u_out = u[first];
     ca.ctl = ctl;
-    CFDJ_HIP(hipFuncSetAttribute(reinterpret_cast<const void*>(mg_coarse_kernel),
-                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)coarse_lds));
+    if (ca_rcp)  // exact reciprocals in place of the divisors
+      for (int c = 0; c < ca.n; ++c) {
+        ca.dx2[c] = 1.0 / ca.dx2[c];
+        ca.dy2[c] = 1.0 / ca.dy2[c];
+        ca.dd[c] = 1.0 / ca.dd[c];
+      }
+    CFDJ_HIP(hipFuncSetAttribute(
+        ca_rcp ? reinterpret_cast<const void*>(mg_coarse_kernel<true>)
+               : reinterpret_cast<const void*>(mg_coarse_kernel<false>),
+        hipFuncAttributeMaxDynamicSharedMemorySize, (int)coarse_lds));
     kc = first;
   }
 
@@ -1018,12 +1048,7 @@ struct Multigrid {
       const double* in = ucur(l);
       flip[l] ^= 1;
       double* out = ucur(l);
-      auto pow2 = [](double d) {
-        int e = 0;
-        const double m = std::frexp(std::fabs(d), &e);
-        return m == 0.5 && e > -500 && e < 500;
-      };
-      const bool rcp = pow2(dx2) && pow2(dy2) && pow2(dd);
+      const bool rcp = exact_pow2(dx2) && exact_pow2(dy2) && exact_pow2(dd);
       const double a = rcp ? 1.0 / dx2 : dx2, b = rcp ? 1.0 / dy2 : dy2, c = rcp ? 1.0 / dd : dd;
       const MgDescArgs da = desc ? *desc : MgDescArgs{};
       if (desc && desc->part) {
@@ -1125,7 +1150,10 @@ struct Multigrid {
       }
       if (next) restrict_to(l + 1);
     }
-    if (kc < nlev) hipLaunchKernelGGL(mg_coarse_kernel, dim3(1), dim3(1024), coarse_lds, st, ca);
+    if (kc < nlev) {
+      if (ca_rcp) hipLaunchKernelGGL(mg_coarse_kernel<true>, dim3(1), dim3(1024), coarse_lds, st, ca);
+      else hipLaunchKernelGGL(mg_coarse_kernel<false>, dim3(1), dim3(1024), coarse_lds, st, ca);
+    }
     for (int k = (kc < nlev ? kc : nlev - 1); k >= 1; --k) smooth(k - 1, v3, k);
     CFDJ_HIP(hipGetLastError());
     for (int l = 0; l < nlev; ++l)
