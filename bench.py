@@ -281,7 +281,13 @@ def main():
     value = cells * args.steps / elapsed / 1e6
     ms_step = elapsed * 1e3 / max(args.steps, 1)
     local_cells = cells / n_gpus
-    kname = "vm_stage_kernel"
+    kname = "vm_stage"
+    # the row-group form runs where the row length is a multiple of 512, the slab's row count
+    # even and no column partial sums are wanted (the substructured y-slab Poisson wants them)
+    rows_local = ny // max(n_gpus, args.virtual or 1)
+    tile = (nx % 512 == 0 and rows_local % 2 == 0 and h.poisson() != "schur"
+            and not args.rows_per_wave)
+    stage_kernel = "vm_stage_tile_kernel<1..3>" if tile else "vm_stage_kernel<1..3>"
     # Roofline of the stage kernels from their IN-STEP launch times: HIP events around every
     # stage-kernel launch of the instrumented timed region (the kernels run in the step's
     # own sequence, between the Poisson passes), algorithmic bytes 24 / 32 / 32 per cell
@@ -310,7 +316,7 @@ def main():
         iso_alg = sum(k["alg_bytes"] for k in st) / 3.0
         iso = iso_alg / (iso_us * 1e-6) / 1e9
     roofline = {
-        "kernel": "vm_stage_kernel (fused Arakawa J + 5-pt Laplacian + RK3 stage)",
+        "kernel": stage_kernel + " (fused Arakawa J + 5-pt Laplacian + RK3 stage)",
         "bound": "hbm",
         "achieved": round(stage_gbs, 1) if stage_gbs else None,
         "peak": HBM_PEAK_GBS,
@@ -327,7 +333,7 @@ def main():
         "source": source,
     }
     pmc = load_pmc(nx)
-    if pmc and pmc.get("stage_kernel", "vm_stage_kernel") == kname:
+    if pmc:
         roofline["traffic"] = pmc["stage_bytes_per_launch"]
         roofline["traffic_source"] = pmc["source"]
     step_gbs = STEP_BYTES_PER_CELL * local_cells * args.steps / elapsed / 1e9

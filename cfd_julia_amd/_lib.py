@@ -22,7 +22,7 @@ ERR_NAMES = {-1: "CFDJ_ERR_ARG", -2: "CFDJ_ERR_HIP", -3: "CFDJ_ERR_ROCFFT",
 K_STAGE, K_FFT_FWD, K_DIVIDE, K_FFT_INV, K_COMM, K_COUNT = range(6)
 K_NAMES = ("stage", "fft_fwd", "divide", "fft_inv", "comm")
 # cfdj_vm_kernel_bench kernel ids (CFDJ_KB_*)
-KB_NAMES = {1: "vm_stage_kernel<1>", 2: "vm_stage_kernel<2>", 3: "vm_stage_kernel<3>",
+KB_NAMES = {1: "vm_stage<1>", 2: "vm_stage<2>", 3: "vm_stage<3>",
             4: "rows_fwd_kernel", 5: "cols_kernel", 6: "rows_inv_kernel"}
 POISSON_AUTO, POISSON_ROCFFT, POISSON_FUSED, POISSON_SCHUR = 0, 1, 2, 3
 SYMBOL_FD, SYMBOL_SPECTRAL = 0, 1

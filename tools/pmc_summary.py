@@ -21,7 +21,7 @@ def per_kernel(path, counter):
         if r["Counter_Name"] != counter:
             continue
         name = r["Kernel_Name"]
-        m = re.search(r"(vm_stage_kernel<\d>|rows_fwd_kernel<\d+>|cols_kernel<\d+>|"
+        m = re.search(r"(vm_stage_tile_kernel<\d>|vm_stage_kernel<\d>|rows_fwd_kernel<\d+>|cols_kernel<\d+>|"
                       r"rows_inv_kernel<\d+>|divide_kernel|\w+kernel\w*)", name)
         vals[m.group(1) if m else name[:60]].append(float(r["Counter_Value"]) * 1024.0)
     return {k: sum(v) / len(v) for k, v in vals.items()}
@@ -43,8 +43,8 @@ def main():
         wr = write.get(k, 0.0)
         kernels[k] = {"read_bytes": round(rd), "write_bytes": round(wr),
                       "hbm_bytes": round(rd + wr)}
-    stage = [v["hbm_bytes"] for k, v in kernels.items() if k.startswith("vm_stage_kernel<")
-             and k != "vm_stage_kernel<0>"]
+    stage = [v["hbm_bytes"] for k, v in kernels.items()
+             if k.startswith(("vm_stage_kernel<", "vm_stage_tile_kernel<")) and not k.endswith("<0>")]
     out = {
         "nx": a.nx,
         "label": a.label,
