@@ -39,11 +39,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "MLUPS (cell-updates/s) + achieved HBM GB/s, 4096² vortex-merger RK3 step"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
-# Algorithmic HBM bytes per cell (SURVEY.md §8d): stage kernels 24 + 32 + 32 per step,
+# Algorithmic HBM bytes per cell: stage kernels 24 + 32 + 32 per step,
 # Poisson 32 per solve (D2Z read 8 + write ~8, Z2D read ~8 + write 8; divide fused).
 STAGE_BYTES_PER_CELL_STEP = 24 + 32 + 32
 STEP_BYTES_PER_CELL = 184
-# per-kernel algorithmic bytes per cell (DESIGN.md §4) for cfdj_vm_kernel_bench ids:
+# per-kernel algorithmic bytes per cell for cfdj_vm_kernel_bench ids:
 # stages read w (+ wn) and psi and write the stage output; each fused Poisson pass reads
 # and writes 8 B per cell (real field or half spectrum)
 KB_BYTES_PER_CELL = {1: 24, 2: 32, 3: 32, 4: 16, 5: 16, 6: 16}

@@ -1,7 +1,7 @@
 // libcfdj.so host side: handles, rocFFT plans, RCCL communicator, the RK3 step driver and
 // the extern "C" ABI declared in include/cfdj.h.
 //
-// Device data layout (DESIGN.md §3): every field is a dense nx-by-rows fp64 block, x
+// Device data layout: every field is a dense nx-by-rows fp64 block, x
 // contiguous (the reference's column-major first index), pitch nx.  No ghost layers are
 // stored: the periodic wrap in x is modular indexing inside the stage kernel, the wrap /
 // halo in y is a pair of row pointers (on one GPU: the slab's own last / first row; on
@@ -807,7 +807,7 @@ cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int
   h->nranks = nranks;
   h->rank = rank;
   // rows per wavefront: keep >= ~8 waves per CU at the benchmark sizes
-  h->rows_per_wave = ny / nranks >= 2048 ? 32 : 8;  // r01 sweep: 32 best at 4096^2
+  h->rows_per_wave = ny / nranks >= 2048 ? 32 : 8;  // measured sweep: 32 best at 4096^2
   CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   if (mode == Mode::Virtual) {
     h->slabs.resize(nranks);

@@ -189,7 +189,7 @@ bool dst_poisson_supported(int nx, int ny);
 int dst_rows_grid(int nx, int ny, int ncu);
 void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
 
-// Substructured y-solve of the y-slab Poisson path (schur.hip, DESIGN.md §5): per x-mode
+// Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row
 // per rank (row 0 of each slab); interior blocks by DST-I (odd-extension FFT of length
 // 2 rl in LDS), separators by a P x P circulant system from the gathered traces.

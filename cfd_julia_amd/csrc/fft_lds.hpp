@@ -155,7 +155,7 @@ __device__ __forceinline__ double fd_symbol(double ax, double cc, double cy) {
 // 1/d for the spectral divide: v_rcp_f64 refined by two Newton steps (|rel. error| below
 // 2^-52 before the final rounding), i.e. within an ulp of the correctly rounded quotient
 // the reference's `e / (...)` (Common.jl:121) forms.  Two true fp64 divisions per complex
-// element cost the column pass 15 us of 81 at 4096^2 (r02, cols_kernel variants); d is a
+// element cost the column pass 15 us of 81 at 4096^2 (measured on cols_kernel variants); d is a
 // normal number here (|d| >= ~1e-7 for grids up to 16384^2, never 0 or denormal).
 __device__ __forceinline__ double recip_nr(double d) {
   double r = __builtin_amdgcn_rcp(d);

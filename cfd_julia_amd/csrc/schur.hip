@@ -1,4 +1,4 @@
-// Substructured y-solve of the multi-GPU (y-slab) FFT Poisson path (DESIGN.md §5).
+// Substructured y-solve of the multi-GPU (y-slab) FFT Poisson path.
 //
 // Common.jl:97-125 divides the 2-D spectrum by D(m, k) = aa + bb cos kx_m + cc cos ky_k.
 // After the real FFT along x (rows_fwd_kernel, local to a slab), each x-mode m >= 1 needs

@@ -1,4 +1,4 @@
-// Spectral-space NS2D solvers of the reference (SURVEY.md §8(f) rank 4):
+// Spectral-space NS2D solvers of the reference:
 //   20_NS2D_Hybrid_Solver/hybrid.jl                         (CFDJ_SPEC_HYBRID)
 //   22_NS2D_PseudoSpectral_23_Rule/pseudospectral_23_rule.jl (CFDJ_SPEC_PS23)
 //   21_NS2D_PseudoSpectral_32_Rule/pseudospectral_32_rule.jl (CFDJ_SPEC_PS32)

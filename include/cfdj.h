@@ -18,7 +18,6 @@
  *   - one host thread per handle at a time.
  *
  * Julia binding: julia/CFDJ.jl.  Python binding: cfd_julia_amd/_lib.py (ctypes).
- * See INTEGRATION.md.
  */
 #ifndef CFDJ_H_
 #define CFDJ_H_

@@ -1,7 +1,7 @@
 """TEST INFRASTRUCTURE ONLY -- never imported by the product path (cfd_julia_amd/).
 
-CPU restatement of the multi-GPU Poisson decomposition that libcfdj.so runs on y-slabs
-(DESIGN.md §5): the reference's periodic FD-FFT solve (Common.jl:97-125, restated in
+CPU restatement of the multi-GPU Poisson decomposition that libcfdj.so runs on y-slabs:
+the reference's periodic FD-FFT solve (Common.jl:97-125, restated in
 vm_oracle.fps) rewritten as
 
   1. real FFT along x (local to a y-slab);

@@ -1,6 +1,6 @@
 """CPU restatement of the y-slab decomposed vortex-merger step (TEST INFRASTRUCTURE ONLY).
 
-The reference is single-process (SURVEY.md §2: no parallelism of any kind).  This module
+The reference is single-process (no parallelism of any kind).  This module
 restates, in NumPy, the decomposition libcfdj.so implements for multi-GPU runs
 (cfd_julia_amd/csrc/cfdj_api.hip: cfdj_vm::poisson / halo / alltoall, pack/unpack
 kernels) so the CPU test suite can check its index arithmetic over real process groups

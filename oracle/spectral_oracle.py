@@ -1,6 +1,6 @@
 """CPU oracle: NumPy/SciPy restatement of the reference's spectral-space NS2D solvers,
 `20_NS2D_Hybrid_Solver/hybrid.jl`, `21_NS2D_PseudoSpectral_32_Rule/pseudospectral_32_rule.jl`
-and `22_NS2D_PseudoSpectral_23_Rule/pseudospectral_23_rule.jl` (SURVEY.md §8(f) rank 4).
+and `22_NS2D_PseudoSpectral_23_Rule/pseudospectral_23_rule.jl`.
 
 TEST INFRASTRUCTURE ONLY.  Only `tests/` may import this module, as the checker of
 libcfdj.so's `cfdj_spec_*` handle; the product path never imports or calls it.
@@ -18,7 +18,7 @@ d_k = α_k (.5Δt k² / re); they differ only in `jacobian` (jf = fft(-J(w, ψ))
 Complex arrays throughout, `real(ifft(...))` as written (the reference never assumes
 Hermitian symmetry, and its ε at kx[1] and its Nyquist derivatives are not Hermitian).
 
-Parity pinning: the reference cannot run here (no `julia`, SURVEY.md §0.3) and ships no
+Parity pinning: the reference cannot run here (no `julia`) and ships no
 output for these scripts, so this restatement is pinned by known answers instead:
   * Taylor-Green (tgv.jl:82-90's ω = 2n cos(nx) cos(ny)): the Jacobian is zero (ω = 2n²ψ
     is a function of ψ), so every solver must reproduce the scheme's exact viscous decay

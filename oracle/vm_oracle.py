@@ -5,7 +5,7 @@ TEST INFRASTRUCTURE ONLY.  Only `tests/`, `__graft_entry__.smoke()` and `bench.p
 `cpu_baseline` leg may import this module, and only as the checker / the timed CPU
 baseline.  The product path (`cfd_julia_amd`, `libcfdj.so`) never imports or calls it.
 
-Parity pinning (SURVEY.md §8c): the Julia reference cannot run in this image (no `julia`,
+Parity pinning: the Julia reference cannot run in this image (no `julia`,
 unregistered `Unroll`/`Utils` deps, unpinned FFTW.jl).  This restatement is pinned by
   * the only published numbers of the reference: the FD-FFT Poisson L2 errors hard-coded
     at `13_Poisson_Solver_FFT_Spectral/specrtral_vs_FDM/order.jl:11` (fft_p.jl MMS,

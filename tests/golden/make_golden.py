@@ -1,6 +1,6 @@
 """Generate the golden fixtures under tests/golden/ from the CPU oracle.
 
-The reference (Julia) cannot run in this image (SURVEY.md §0.3: no julia binary,
+The reference (Julia) cannot run in this image (no julia binary,
 unregistered Unroll/Utils deps), so the fixtures are produced by oracle/vm_oracle.py,
 which is itself pinned to the reference's published numbers (order.jl:10-11) and the
 analytic TGV decay (tgv.jl:82-90) -- see tests/test_oracle.py.  Re-run with

@@ -1,4 +1,4 @@
-"""Text field formats (SURVEY §8f rank 3): vm.jl:81-85 / 130-146 and
+"""Text field formats: vm.jl:81-85 / 130-146 and
 lid_driven_cavity.jl:201-214, read back as 19/plotting.jl:14-31 does (readdlm + reshape).
 
 Julia number formatting pinned by known answers of Base.show for Float64 (plain for

@@ -18,7 +18,7 @@ def test_ftcs_bit_exact_vs_oracle():
 
 @pytest.mark.parametrize("dx,dt", [(0.025, 0.0025), (2.0 / 1024, 2.0 ** -16)])
 def test_ftcs_analytic_decay(dx, dt):
-    # C1: nx = 1024 needs beta <= 0.5; dt = 2^-16 gives beta = 0.405 (SURVEY §8a)
+    # C1: nx = 1024 needs beta <= 0.5; dt = 2^-16 gives beta = 0.405
     from cfd_julia_amd import ftcs
 
     l2, linf = ftcs.main(dx=dx, dt=dt, t=1.0 if dx > 0.01 else 0.05)

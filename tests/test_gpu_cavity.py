@@ -1,4 +1,4 @@
-"""GPU parity of the secondary paths (SURVEY §8a P1): lid-driven cavity and multigrid.
+"""GPU parity of the secondary paths: lid-driven cavity and multigrid.
 
 Tolerances: cavity rhs bit-exact given (w, s); fps_sine within 1e-12 max|s| (DST via the
 odd-extension FFT vs scipy's DST-I); cavity fields after K steps within 1e-10; multigrid:

@@ -2,7 +2,7 @@
 same columns as rocprofv3's `--stats` kernel_stats.csv (Name, Calls, TotalDurationNs,
 AverageNs, Percentage).  ROCm 7.2's rocprofv3 writes the rocpd SQLite format by default.
 
-usage: python tools/rocpd_stats.py gpurun_out/prof/run_results.db profiles/r01/x.csv
+usage: python tools/rocpd_stats.py gpurun_out/prof/run_results.db profiles/x.csv
 """
 import csv
 import sqlite3
