@@ -124,15 +124,18 @@ __device__ __forceinline__ void dft(double2* v) {
   }
 }
 
-// Stockham plan of a length-L transform: radix-16 stages, then one remainder stage.
-template <int L>
+// Stockham plan of a length-L transform with NV values per thread (16, or 8 where more
+// wavefronts per transform are wanted): radix-NV stages, then one remainder stage.
+template <int L, int NV = 16>
 struct Plan {
+  static_assert(NV == 16 || NV == 8, "values per thread");
   static constexpr int LOG = ilog2(L);
-  static constexpr int N16 = LOG / 4;
-  static constexpr int REM = 1 << (LOG % 4);
-  static constexpr int NSTAGES = N16 + (REM > 1 ? 1 : 0);
-  static constexpr int T = L / 16;  // threads per transform
-  static constexpr int radix(int s) { return s < N16 ? 16 : REM; }
+  static constexpr int LNV = ilog2(NV);
+  static constexpr int NFULL = LOG / LNV;
+  static constexpr int REM = 1 << (LOG % LNV);
+  static constexpr int NSTAGES = NFULL + (REM > 1 ? 1 : 0);
+  static constexpr int T = L / NV;  // threads per transform
+  static constexpr int radix(int s) { return s < NFULL ? NV : REM; }
   static constexpr int ns(int s) { return s == 0 ? 1 : ns(s - 1) * radix(s - 1); }
   static constexpr int PAD = L + L / 16;  // LDS elements per transform (1 pad per 16)
   static constexpr int ROWSTRIDE = PAD;  // rows kernels: row stride (= 0 mod 64 banks)
@@ -243,44 +246,46 @@ __device__ __forceinline__ void butterfly(double2* v, const Tw<L, R, NS>& t) {
   dft<R, DIR>(v);
 }
 
-// Stage S of the plan on the thread's 16 registers (16/R butterflies of radix R):
-// inputs v[b*R + r] = element (j_b + r*L/R), j_b = tid + b*T.
-template <int L, int S>
+// Stage S of the plan on the thread's NV registers (NV/R butterflies of radix R):
+// inputs v[b*R + r] = element (j_b + r*L/R), j_b = tid + b*T.  NV is deduced from the
+// register array wherever one is passed.
+template <int L, int S, int NV = 16>
 struct StageTw {
-  static constexpr int R = Plan<L>::radix(S);
-  static constexpr int NS = Plan<L>::ns(S);
-  Tw<L, R, NS> t[16 / R];
+  static constexpr int R = Plan<L, NV>::radix(S);
+  static constexpr int NS = Plan<L, NV>::ns(S);
+  Tw<L, R, NS> t[NV / R];
 };
-template <int L, int S, class TW>
-__device__ __forceinline__ StageTw<L, S> stage_tw(int tid, const TW& tw) {
-  StageTw<L, S> st;
+template <int L, int S, class TW, int NV = 16>
+__device__ __forceinline__ StageTw<L, S, NV> stage_tw(int tid, const TW& tw) {
+  using ST = StageTw<L, S, NV>;
+  ST st;
 #pragma unroll
-  for (int b = 0; b < 16 / StageTw<L, S>::R; ++b)
-    st.t[b] = load_tw<L, StageTw<L, S>::R, StageTw<L, S>::NS, TW>(tid + b * Plan<L>::T, tw);
+  for (int b = 0; b < NV / ST::R; ++b)
+    st.t[b] = load_tw<L, ST::R, ST::NS, TW>(tid + b * Plan<L, NV>::T, tw);
   return st;
 }
-template <int L, int S, int DIR>
-__device__ __forceinline__ void stage_regs(double2 (&v)[16], const StageTw<L, S>& st) {
-  constexpr int R = Plan<L>::radix(S);
-  constexpr int NS = Plan<L>::ns(S);
+template <int L, int S, int DIR, int NV>
+__device__ __forceinline__ void stage_regs(double2 (&v)[NV], const StageTw<L, S, NV>& st) {
+  constexpr int R = Plan<L, NV>::radix(S);
+  constexpr int NS = Plan<L, NV>::ns(S);
 #pragma unroll
-  for (int b = 0; b < 16 / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);
+  for (int b = 0; b < NV / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);
 }
-template <int L, int S, int DIR, class TW>
-__device__ __forceinline__ void stage_regs(double2 (&v)[16], int tid, const TW& tw) {
-  stage_regs<L, S, DIR>(v, stage_tw<L, S, TW>(tid, tw));
+template <int L, int S, int DIR, class TW, int NV>
+__device__ __forceinline__ void stage_regs(double2 (&v)[NV], int tid, const TW& tw) {
+  stage_regs<L, S, DIR>(v, stage_tw<L, S, TW, NV>(tid, tw));
 }
 
 // Stage input / output positions.
-template <int L, int S>
+template <int L, int S, int NV = 16>
 __device__ __forceinline__ int in_pos(int tid, int b, int r) {
-  using P = Plan<L>;
+  using P = Plan<L, NV>;
   constexpr int R = P::radix(S);
   return tid + b * P::T + r * (L / R);
 }
-template <int L, int S>
+template <int L, int S, int NV = 16>
 __device__ __forceinline__ int out_pos(int tid, int b, int r) {
-  using P = Plan<L>;
+  using P = Plan<L, NV>;
   constexpr int R = P::radix(S);
   constexpr int NS = P::ns(S);
   const int j = tid + b * P::T;
@@ -290,31 +295,31 @@ __device__ __forceinline__ int out_pos(int tid, int b, int r) {
 // LDS element p of a transform lives at buf[IL * padx(p)]: IL = 1 for one transform per
 // buffer (rows), IL = 2 for the two interleaved columns of a tile (cols), so consecutive
 // lanes -- (tid, c) pairs -- touch consecutive 16-B slots.
-template <int L, int S, int IL = 1>
-__device__ __forceinline__ void lds_write(double2* buf, const double2 (&v)[16], int tid) {
-  constexpr int R = Plan<L>::radix(S);
+template <int L, int S, int IL = 1, int NV>
+__device__ __forceinline__ void lds_write(double2* buf, const double2 (&v)[NV], int tid) {
+  constexpr int R = Plan<L, NV>::radix(S);
 #pragma unroll
-  for (int b = 0; b < 16 / R; ++b)
+  for (int b = 0; b < NV / R; ++b)
 #pragma unroll
-    for (int r = 0; r < R; ++r) buf[IL * padx(out_pos<L, S>(tid, b, r))] = v[b * R + r];
+    for (int r = 0; r < R; ++r) buf[IL * padx(out_pos<L, S, NV>(tid, b, r))] = v[b * R + r];
 }
-template <int L, int S, int IL = 1>
-__device__ __forceinline__ void lds_read(const double2* buf, double2 (&v)[16], int tid) {
-  constexpr int R = Plan<L>::radix(S);
+template <int L, int S, int IL = 1, int NV>
+__device__ __forceinline__ void lds_read(const double2* buf, double2 (&v)[NV], int tid) {
+  constexpr int R = Plan<L, NV>::radix(S);
 #pragma unroll
-  for (int b = 0; b < 16 / R; ++b)
+  for (int b = 0; b < NV / R; ++b)
 #pragma unroll
-    for (int r = 0; r < R; ++r) v[b * R + r] = buf[IL * padx(in_pos<L, S>(tid, b, r))];
+    for (int r = 0; r < R; ++r) v[b * R + r] = buf[IL * padx(in_pos<L, S, NV>(tid, b, r))];
 }
 
 // Middle stages S0..NSTAGES-1 (each: read LDS, barrier, compute, write LDS, barrier).
 // The caller has written stage S0-1's output to LDS and synchronised.
-template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW>
-__device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[16], int tid,
+template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW, int NV>
+__device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[NV], int tid,
                                            const TW& tw) {
-  using P = Plan<L>;
+  using P = Plan<L, NV>;
   if constexpr (S < P::NSTAGES) {
-    const StageTw<L, S> st = stage_tw<L, S, TW>(tid, tw);
+    const StageTw<L, S, NV> st = stage_tw<L, S, TW, NV>(tid, tw);
     lds_read<L, S, IL>(buf, v, tid);
     __syncthreads();
     stage_regs<L, S, DIR>(v, st);
@@ -322,38 +327,38 @@ __device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[16], int t
       lds_write<L, S, IL>(buf, v, tid);
       __syncthreads();
     }
-    run_stages<L, S + 1, DIR, LAST_TO_LDS, IL, TW>(buf, v, tid, tw);
+    run_stages<L, S + 1, DIR, LAST_TO_LDS, IL>(buf, v, tid, tw);
   }
 }
 
 // Component-wise exchange: the transform's LDS buffer holds ONE double per element (half
 // the footprint of the complex buffer, so more workgroups fit a CU) and the real and the
 // imaginary parts pass through it one after the other.  C = 0: real, 1: imaginary.
-template <int L, int S, int C>
-__device__ __forceinline__ void lds_write_half(double* buf, const double2 (&v)[16], int tid) {
-  constexpr int R = Plan<L>::radix(S);
+template <int L, int S, int C, int NV>
+__device__ __forceinline__ void lds_write_half(double* buf, const double2 (&v)[NV], int tid) {
+  constexpr int R = Plan<L, NV>::radix(S);
 #pragma unroll
-  for (int b = 0; b < 16 / R; ++b)
+  for (int b = 0; b < NV / R; ++b)
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      buf[padx(out_pos<L, S>(tid, b, r))] = C ? v[b * R + r].y : v[b * R + r].x;
+      buf[padx(out_pos<L, S, NV>(tid, b, r))] = C ? v[b * R + r].y : v[b * R + r].x;
 }
-template <int L, int S, int C>
-__device__ __forceinline__ void lds_read_half(const double* buf, double2 (&v)[16], int tid) {
-  constexpr int R = Plan<L>::radix(S);
+template <int L, int S, int C, int NV>
+__device__ __forceinline__ void lds_read_half(const double* buf, double2 (&v)[NV], int tid) {
+  constexpr int R = Plan<L, NV>::radix(S);
 #pragma unroll
-  for (int b = 0; b < 16 / R; ++b)
+  for (int b = 0; b < NV / R; ++b)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const double t = buf[padx(in_pos<L, S>(tid, b, r))];
+      const double t = buf[padx(in_pos<L, S, NV>(tid, b, r))];
       if constexpr (C) v[b * R + r].y = t;
       else v[b * R + r].x = t;
     }
 }
 // Outputs of stage S-1 (in v) -> inputs of stage S (in v).  The leading barrier protects the
 // buffer from readers of the previous exchange.
-template <int L, int S>
-__device__ __forceinline__ void exchange_half(double* buf, double2 (&v)[16], int tid) {
+template <int L, int S, int NV>
+__device__ __forceinline__ void exchange_half(double* buf, double2 (&v)[NV], int tid) {
   __syncthreads();
   lds_write_half<L, S - 1, 0>(buf, v, tid);
   __syncthreads();
@@ -364,32 +369,32 @@ __device__ __forceinline__ void exchange_half(double* buf, double2 (&v)[16], int
   lds_read_half<L, S, 1>(buf, v, tid);
 }
 // Stages S..NSTAGES-1 on stage S-1's outputs held in v; the last stage's outputs stay in v.
-template <int L, int S, int DIR, class TW>
-__device__ __forceinline__ void run_stages_half(double* buf, double2 (&v)[16], int tid,
+template <int L, int S, int DIR, class TW, int NV>
+__device__ __forceinline__ void run_stages_half(double* buf, double2 (&v)[NV], int tid,
                                                 const TW& tw) {
-  using P = Plan<L>;
+  using P = Plan<L, NV>;
   if constexpr (S < P::NSTAGES) {
-    const StageTw<L, S> st = stage_tw<L, S, TW>(tid, tw);
+    const StageTw<L, S, NV> st = stage_tw<L, S, TW, NV>(tid, tw);
     exchange_half<L, S>(buf, v, tid);
-    // keep the twiddle powers (30 doubles) from being formed before the exchange, where
-    // both the old and the new halves of v are live
+    // keep the twiddle powers from being formed before the exchange, where both the old
+    // and the new halves of v are live
     __builtin_amdgcn_sched_barrier(0);
     stage_regs<L, S, DIR>(v, st);
-    run_stages_half<L, S + 1, DIR, TW>(buf, v, tid, tw);
+    run_stages_half<L, S + 1, DIR>(buf, v, tid, tw);
   }
 }
 
 // run_stages for workgroups whose transform groups are not all busy: a group with
 // act == false keeps every barrier (they are workgroup-wide, and stay outside the
 // branches: act may differ inside one wavefront when T < 64) but touches no LDS.
-template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW>
-__device__ __forceinline__ void run_stages_if(double2* buf, double2 (&v)[16], int tid,
+template <int L, int S, int DIR, bool LAST_TO_LDS, int IL = 1, class TW, int NV>
+__device__ __forceinline__ void run_stages_if(double2* buf, double2 (&v)[NV], int tid,
                                               const TW& tw, bool act) {
-  using P = Plan<L>;
+  using P = Plan<L, NV>;
   if constexpr (S < P::NSTAGES) {
-    StageTw<L, S> st;
+    StageTw<L, S, NV> st;
     if (act) {
-      st = stage_tw<L, S, TW>(tid, tw);
+      st = stage_tw<L, S, TW, NV>(tid, tw);
       lds_read<L, S, IL>(buf, v, tid);
     }
     __syncthreads();
@@ -398,21 +403,21 @@ __device__ __forceinline__ void run_stages_if(double2* buf, double2 (&v)[16], in
       if (act) lds_write<L, S, IL>(buf, v, tid);
       __syncthreads();
     }
-    run_stages_if<L, S + 1, DIR, LAST_TO_LDS, IL, TW>(buf, v, tid, tw, act);
+    run_stages_if<L, S + 1, DIR, LAST_TO_LDS, IL>(buf, v, tid, tw, act);
   }
 }
 
 // After the forward transform's last stage a thread holds elements (j_b + r*NS), the same
 // set the inverse transform's stage 0 reads (tid + T*r'), in a different register order:
-// r' = b + (16/R_last)*r.  fwd_to_inv permutes the registers accordingly.
-template <int M>
-__device__ __forceinline__ void fwd_to_inv(const double2 (&a)[16], double2 (&v)[16]) {
-  using P = Plan<M>;
+// r' = b + (NV/R_last)*r.  fwd_to_inv permutes the registers accordingly.
+template <int M, int NV>
+__device__ __forceinline__ void fwd_to_inv(const double2 (&a)[NV], double2 (&v)[NV]) {
+  using P = Plan<M, NV>;
   constexpr int RL = P::radix(P::NSTAGES - 1);
 #pragma unroll
-  for (int b = 0; b < 16 / RL; ++b)
+  for (int b = 0; b < NV / RL; ++b)
 #pragma unroll
-    for (int r = 0; r < RL; ++r) v[b + (16 / RL) * r] = a[b * RL + r];
+    for (int r = 0; r < RL; ++r) v[b + (NV / RL) * r] = a[b * RL + r];
 }
 
 // Persistent work split: `nb` resident workgroups (a multiple of 8) process items [0, n).

@@ -243,14 +243,41 @@ __device__ __forceinline__ double2 packed_divide(double2 Z, double2 Zp, int k, d
   return make_double2((A2.x - B2.y) * da.scale, (A2.y + B2.x) * da.scale);
 }
 
-template <int M>
-__device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __restrict__ col,
+template <int M, int NV>
+__device__ __forceinline__ void load_col(double2 (&a)[NV], const double2* __restrict__ col,
                                          int tid, int rl_log2, unsigned seg) {
-  constexpr int R0 = Plan<M>::radix(0);
+  constexpr int R0 = Plan<M, NV>::radix(0);
 #pragma unroll
-  for (int b = 0; b < 16 / R0; ++b)
+  for (int b = 0; b < NV / R0; ++b)
 #pragma unroll
-    for (int r = 0; r < R0; ++r) a[b * R0 + r] = col[col_off(in_pos<M, 0>(tid, b, r), rl_log2, seg)];
+    for (int r = 0; r < R0; ++r)
+      a[b * R0 + r] = col[col_off(in_pos<M, 0, NV>(tid, b, r), rl_log2, seg)];
+}
+
+// The column kernel's shape: NV values per thread (M / NV threads per column) and the LDS
+// exchange, component-wise (HALF: one double per element) or complex.
+#ifndef CFDJ_COLS_NV
+#define CFDJ_COLS_NV 16
+#endif
+#ifndef CFDJ_COLS_HALF
+#define CFDJ_COLS_HALF 1
+#endif
+constexpr int kColsNV = CFDJ_COLS_NV;
+constexpr bool kColsHalf = CFDJ_COLS_HALF != 0;
+
+// Stages 0.. of a length-M transform on v; the last stage's outputs stay in v.  The LDS
+// buffer may still be read by the previous transform's last stage.
+template <int M, int DIR, bool HALF, class TW, int NV>
+__device__ __forceinline__ void col_fft(void* lds, double2 (&v)[NV], int tid, const TW& tw) {
+  stage_regs<M, 0, DIR>(v, tid, tw);
+  if constexpr (HALF) {
+    run_stages_half<M, 1, DIR>(static_cast<double*>(lds), v, tid, tw);
+  } else {
+    __syncthreads();
+    lds_write<M, 0>(static_cast<double2*>(lds), v, tid);
+    __syncthreads();
+    run_stages<M, 1, DIR, false>(static_cast<double2*>(lds), v, tid, tw);
+  }
 }
 
 // One column: forward FFT, divide, inverse FFT.  PACKED = the column of slot 0, Z =
@@ -260,25 +287,24 @@ __device__ __forceinline__ void load_col(double2 (&a)[16], const double2* __rest
 // of the whole body (no merge of two versions of the registers), its spectrum goes through
 // the output column in global memory and a rolled loop over the pairs (k, M - k) transforms
 // it in place.
-template <int M, bool MIRROR, bool PACKED>
-__device__ __forceinline__ void cols_column(double* lds, const double2* __restrict__ col,
+template <int M, bool MIRROR, bool PACKED, int NV, bool HALF>
+__device__ __forceinline__ void cols_column(void* lds, const double2* __restrict__ col,
                                             double2* __restrict__ ocol, int m, int tid,
                                             const TwGlobal<M>& twM, const DivArgs& da) {
-  using P = Plan<M>;
+  using P = Plan<M, NV>;
   const double sgn = da.neg ? -1.0 : 1.0;
   constexpr bool mirror = MIRROR;  // symbol not even in ky (ny < nx): a template flag, so
                                   // the square-grid kernel carries no cy_mirror loads
-  double2 a[16];
+  double2 a[NV];
   load_col<M>(a, col, tid, da.rl_log2, da.seg);
-  stage_regs<M, 0, -1>(a, tid, twM);
-  run_stages_half<M, 1, -1>(lds, a, tid, twM);  // last stage stays in registers
+  col_fft<M, -1, HALF>(lds, a, tid, twM);
 
-  double2 v[16];
+  double2 v[NV];
   fwd_to_inv<M>(a, v);  // v[r] = spectrum at k = tid + T*r, natural order
   const double ax = fd_symbol_x(da.aa, da.bb, da.cx[m]);
   if constexpr (!PACKED) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
+    for (int r = 0; r < NV; ++r) {
       const int k = tid + P::T * r;
       const double d = fd_symbol(ax, da.cc, da.cy[k]);
       const double d2 = mirror ? fd_symbol(ax, da.cc, da.cy_mirror[k]) : d;
@@ -287,7 +313,7 @@ __device__ __forceinline__ void cols_column(double* lds, const double2* __restri
     }
   } else {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)] = v[r];
+    for (int r = 0; r < NV; ++r) ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)] = v[r];
     __syncthreads();  // workgroup-scope release / acquire of the global stores
     const double axL = fd_symbol_x(da.aa, da.bb, da.cx[da.L]);
 #pragma unroll 1
@@ -301,28 +327,30 @@ __device__ __forceinline__ void cols_column(double* lds, const double2* __restri
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)];
+    for (int r = 0; r < NV; ++r) v[r] = ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)];
     __syncthreads();  // every reload precedes the final stores to the same column
   }
-  stage_regs<M, 0, 1>(v, tid, twM);
-  run_stages_half<M, 1, 1>(lds, v, tid, twM);
+  col_fft<M, 1, HALF>(lds, v, tid, twM);
   // last inverse stage: outputs j + r*NS are in natural order -> straight to HBM
   constexpr int SL = P::NSTAGES - 1;
   constexpr int RL = P::radix(SL);
 #pragma unroll
-  for (int b = 0; b < 16 / RL; ++b)
+  for (int b = 0; b < NV / RL; ++b)
 #pragma unroll
     for (int r = 0; r < RL; ++r)
-      ocol[col_off(out_pos<M, SL>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
+      ocol[col_off(out_pos<M, SL, NV>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
 }
 
-// Wavefronts per SIMD the column kernel is compiled for (its register cap): one per
-// resident workgroup when a workgroup is 4 wavefronts (M = 4096: LDS allows 4, registers 3).
+// Wavefronts per SIMD the column kernel is compiled for (its register cap): with 16 values
+// per thread one per resident workgroup when a workgroup is 4 wavefronts (M = 4096: LDS
+// allows 4, registers 3); with 8 values per thread, 4.
 template <int M>
-constexpr int cols_waves() { return Plan<M>::T == 256 && M <= 4096 ? 3 : 2; }
+constexpr int cols_waves() {
+  return kColsNV == 8 ? 4 : (Plan<M>::T == 256 && M <= 4096 ? 3 : 2);
+}
 
 template <int M, bool MIRROR>
-__global__ __launch_bounds__(Plan<M>::T)
+__global__ __launch_bounds__((Plan<M, kColsNV>::T))
     __attribute__((amdgpu_waves_per_eu(cols_waves<M>(), cols_waves<M>()))) void cols_kernel(const double2* __restrict__ C,
                                                         double2* __restrict__ Cout,
                                                         const double2* __restrict__ twM_,
@@ -333,9 +361,9 @@ __global__ __launch_bounds__(Plan<M>::T)
   // double per element and the stages exchange real and imaginary parts one after the other
   // (exchange_half), 34 KB at M = 4096 -- three workgroups per CU (the registers' limit)
   // where a complex buffer allows two.
-  using P = Plan<M>;
+  using P = Plan<M, kColsNV>;
   static_assert(P::NSTAGES >= 2, "column length");
-  __shared__ double lds[P::PAD];
+  __shared__ double2 lds[kColsHalf ? (P::PAD + 1) / 2 : P::PAD];
   const TwGlobal<M> twM{twM_};
   const int tid = threadIdx.x;
   const int ml = xcd_remap(blockIdx.x, gridDim.x);
@@ -343,10 +371,10 @@ __global__ __launch_bounds__(Plan<M>::T)
   const double2* col = C + ((size_t)ml << da.rl_log2);
   double2* ocol = Cout + ((size_t)ml << da.rl_log2);
   if (m == 0) {
-    cols_column<M, MIRROR, true>(lds, col, ocol, m, tid, twM, da);
+    cols_column<M, MIRROR, true, kColsNV, kColsHalf>(lds, col, ocol, m, tid, twM, da);
     return;
   }
-  cols_column<M, MIRROR, false>(lds, col, ocol, m, tid, twM, da);
+  cols_column<M, MIRROR, false, kColsNV, kColsHalf>(lds, col, ocol, m, tid, twM, da);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -509,9 +537,9 @@ void launch_cols(const FusedPoissonArgs& a, hipStream_t st) {
              a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, a.m0, a.rl_log2, a.seg};
   double2* out = a.Cout ? a.Cout : a.C;
   if (a.cy_mirror == nullptr)
-    hipLaunchKernelGGL((cols_kernel<M, false>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, out, a.twM, da);
+    hipLaunchKernelGGL((cols_kernel<M, false>), dim3(a.kb), dim3(Plan<M, kColsNV>::T), 0, st, a.C, out, a.twM, da);
   else
-    hipLaunchKernelGGL((cols_kernel<M, true>), dim3(a.kb), dim3(Plan<M>::T), 0, st, a.C, out, a.twM, da);
+    hipLaunchKernelGGL((cols_kernel<M, true>), dim3(a.kb), dim3(Plan<M, kColsNV>::T), 0, st, a.C, out, a.twM, da);
 }
 
 constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
