@@ -189,6 +189,13 @@ bool dst_poisson_supported(int nx, int ny);
 int dst_rows_grid(int nx, int ny, int ncu);
 void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
 
+// In-place 2-D complex FFT of `batch` nx-by-ny arrays (x contiguous) in two passes,
+// unnormalised both ways (fft2d_c2c.hip).  dir < 0 forward, > 0 inverse; twX / twY:
+// exp(-2 pi i k / n) device tables for n = nx, ny.
+bool c2c2d_supported(int nx, int ny);
+void launch_c2c2d(double2* a, int nx, int ny, int batch, int dir, const double2* twX,
+                  const double2* twY, hipStream_t st);
+
 // Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row
 // per rank (row 0 of each slab); interior blocks by DST-I (odd-extension FFT of length

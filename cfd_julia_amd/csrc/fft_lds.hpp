@@ -333,54 +333,56 @@ __device__ __forceinline__ void run_stages(double2* buf, double2 (&v)[NV], int t
 
 // Component-wise exchange: the transform's LDS buffer holds ONE double per element (half
 // the footprint of the complex buffer, so more workgroups fit a CU) and the real and the
-// imaginary parts pass through it one after the other.  C = 0: real, 1: imaginary.
-template <int L, int S, int C, int NV>
+// imaginary parts pass through it one after the other.  C = 0: real, 1: imaginary.  IL as
+// in lds_write: IL transforms interleaved element by element, `buf` offset by the
+// transform's index.
+template <int L, int S, int C, int IL = 1, int NV>
 __device__ __forceinline__ void lds_write_half(double* buf, const double2 (&v)[NV], int tid) {
   constexpr int R = Plan<L, NV>::radix(S);
 #pragma unroll
   for (int b = 0; b < NV / R; ++b)
 #pragma unroll
     for (int r = 0; r < R; ++r)
-      buf[padx(out_pos<L, S, NV>(tid, b, r))] = C ? v[b * R + r].y : v[b * R + r].x;
+      buf[IL * padx(out_pos<L, S, NV>(tid, b, r))] = C ? v[b * R + r].y : v[b * R + r].x;
 }
-template <int L, int S, int C, int NV>
+template <int L, int S, int C, int IL = 1, int NV>
 __device__ __forceinline__ void lds_read_half(const double* buf, double2 (&v)[NV], int tid) {
   constexpr int R = Plan<L, NV>::radix(S);
 #pragma unroll
   for (int b = 0; b < NV / R; ++b)
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      const double t = buf[padx(in_pos<L, S, NV>(tid, b, r))];
+      const double t = buf[IL * padx(in_pos<L, S, NV>(tid, b, r))];
       if constexpr (C) v[b * R + r].y = t;
       else v[b * R + r].x = t;
     }
 }
 // Outputs of stage S-1 (in v) -> inputs of stage S (in v).  The leading barrier protects the
 // buffer from readers of the previous exchange.
-template <int L, int S, int NV>
+template <int L, int S, int IL = 1, int NV>
 __device__ __forceinline__ void exchange_half(double* buf, double2 (&v)[NV], int tid) {
   __syncthreads();
-  lds_write_half<L, S - 1, 0>(buf, v, tid);
+  lds_write_half<L, S - 1, 0, IL>(buf, v, tid);
   __syncthreads();
-  lds_read_half<L, S, 0>(buf, v, tid);
+  lds_read_half<L, S, 0, IL>(buf, v, tid);
   __syncthreads();
-  lds_write_half<L, S - 1, 1>(buf, v, tid);
+  lds_write_half<L, S - 1, 1, IL>(buf, v, tid);
   __syncthreads();
-  lds_read_half<L, S, 1>(buf, v, tid);
+  lds_read_half<L, S, 1, IL>(buf, v, tid);
 }
 // Stages S..NSTAGES-1 on stage S-1's outputs held in v; the last stage's outputs stay in v.
-template <int L, int S, int DIR, class TW, int NV>
+template <int L, int S, int DIR, int IL = 1, class TW, int NV>
 __device__ __forceinline__ void run_stages_half(double* buf, double2 (&v)[NV], int tid,
                                                 const TW& tw) {
   using P = Plan<L, NV>;
   if constexpr (S < P::NSTAGES) {
     const StageTw<L, S, NV> st = stage_tw<L, S, TW, NV>(tid, tw);
-    exchange_half<L, S>(buf, v, tid);
+    exchange_half<L, S, IL>(buf, v, tid);
     // keep the twiddle powers from being formed before the exchange, where both the old
     // and the new halves of v are live
     __builtin_amdgcn_sched_barrier(0);
     stage_regs<L, S, DIR>(v, st);
-    run_stages_half<L, S + 1, DIR>(buf, v, tid, tw);
+    run_stages_half<L, S + 1, DIR, IL>(buf, v, tid, tw);
   }
 }
 

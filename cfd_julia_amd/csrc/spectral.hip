@@ -232,6 +232,23 @@ struct cfdj_spec {
   Plans plans;
   rocfft_plan fwd = nullptr, inv = nullptr;      // nx x ny, batch 1 (in place)
   rocfft_plan inv_b = nullptr, fwd_p = nullptr;  // product grid: batch 2 / 4 inverse, forward
+  // hand-written two-pass transform (fft2d_c2c.hip) on power-of-two grids; the library
+  // plans above stay for the other sizes and for CFDJ_SPEC_FFT=rocfft
+  bool hand_n = false, hand_p = false;           // nx x ny / px x py
+  double2 *tw_n = nullptr, *tw_p = nullptr;      // twiddle tables (nx == ny, px == py)
+  int nb = 2;                                    // arrays in X
+
+  // In-place 2-D transform of `batch` arrays: the library plan `pl` or the hand-written one.
+  void fft2(rocfft_plan pl, double2* buf, bool product_grid, int batch, int dir) {
+    const bool hand = product_grid ? hand_p : hand_n;
+    if (hand) {
+      const int gx = product_grid ? px : nx, gy = product_grid ? py : ny;
+      const double2* tw = product_grid ? tw_p : tw_n;
+      launch_c2c2d(buf, gx, gy, batch, dir, tw, tw, stream);
+    } else {
+      plans.exec(pl, buf, nullptr);
+    }
+  }
 
   size_t n() const { return (size_t)nx * ny; }
   size_t np() const { return (size_t)px * py; }
@@ -243,12 +260,12 @@ struct cfdj_spec {
       hipLaunchKernelGGL(hybrid_prep_kernel, dim3(grid_for(n())), dim3(256), 0, stream, wf, kx,
                          X, nx, ny);
       CFDJ_HIP(hipGetLastError());
-      plans.exec(inv_b, X, nullptr);
+      fft2(inv_b, X, true, nb, 1);
       const double gg = 1.0 / (4.0 * dx * dy), hh = 1.0 / 3.0;
       hipLaunchKernelGGL(hybrid_jac_kernel, dim3(grid_for(n())), dim3(256), 0, stream, X, jf,
                          nx, ny, 1.0 / ((double)nx * ny), gg, hh);
       CFDJ_HIP(hipGetLastError());
-      plans.exec(fwd, jf, nullptr);
+      fft2(fwd, jf, false, 1, -1);
       return;
     }
     const bool r32 = kind == CFDJ_SPEC_PS32;
@@ -258,12 +275,12 @@ struct cfdj_spec {
     hipLaunchKernelGGL(ps_derivs_kernel, dim3(gb), dim3(256), 0, stream, wf, kx, X, nx, ny, px,
                        py, r32 ? 1 : 0, tx0, tx1, ty0, ty1, sc, sd);
     CFDJ_HIP(hipGetLastError());
-    plans.exec(inv_b, X, nullptr);
+    fft2(inv_b, X, true, nb, 1);
     double2* P = r32 ? J : jf;
     hipLaunchKernelGGL(ps_product_kernel, dim3(gb), dim3(256), 0, stream, X, P, np(),
                        1.0 / sc);
     CFDJ_HIP(hipGetLastError());
-    plans.exec(r32 ? fwd_p : fwd, P, nullptr);
+    fft2(r32 ? fwd_p : fwd, P, r32, 1, -1);
     if (r32) {
       hipLaunchKernelGGL(ps_unpad_kernel, dim3(grid_for(n())), dim3(256), 0, stream, J, jf, nx,
                          ny, px, py, sd, sc);
@@ -295,6 +312,8 @@ struct cfdj_spec {
   ~cfdj_spec() {
     if (stream) (void)hipStreamSynchronize(stream);
     plans.destroy();
+    if (tw_p != tw_n) dfree(tw_p);
+    dfree(tw_n);
     for (double2** p : {&wn, &w1, &w2, &jn, &j1, &j2, &X, &J}) dfree(*p);
     dfree(kx);
     dfree(field);
@@ -344,6 +363,13 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
       CFDJ_HIP(hipMemset(*p, 0, n * sizeof(double2)));
     }
     const int nb = kind == CFDJ_SPEC_HYBRID ? 2 : 4;
+    h->nb = nb;
+    const char* fe = std::getenv("CFDJ_SPEC_FFT");
+    const bool want_hand = !(fe && std::strcmp(fe, "rocfft") == 0);
+    h->hand_n = want_hand && c2c2d_supported(nx, ny);
+    h->hand_p = want_hand && c2c2d_supported(h->px, h->py);
+    if (h->hand_n) h->tw_n = twiddle_table(nx);
+    if (h->hand_p) h->tw_p = (h->px == nx && h->tw_n) ? h->tw_n : twiddle_table(h->px);
     h->X = dalloc<double2>((size_t)nb * np);
     if (kind == CFDJ_SPEC_PS32) h->J = dalloc<double2>(np);
     h->field = dalloc<double>((size_t)(nx + 1) * (ny + 1));
@@ -376,7 +402,7 @@ int cfdj_spec_upload(cfdj_spec* h, const double* wn, long ldw) {
     hipLaunchKernelGGL(to_complex_kernel, dim3(grid_for(h->n())), dim3(256), 0, h->stream,
                        h->field, (long)(nx + 1), h->wn, nx, ny);
     CFDJ_HIP(hipGetLastError());
-    h->plans.exec(h->fwd, h->wn, nullptr);
+    h->fft2(h->fwd, h->wn, false, 1, -1);
     CFDJ_HIP(hipMemsetAsync(h->wn, 0, sizeof(double2), h->stream));
     CFDJ_HIP(hipStreamSynchronize(h->stream));
   });
@@ -401,7 +427,7 @@ int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu) {
     const int nx = h->nx, ny = h->ny;
     CFDJ_HIP(hipMemcpyAsync(h->j2, h->wn, h->n() * sizeof(double2), hipMemcpyDeviceToDevice,
                             h->stream));  // j2 is scratch between steps
-    h->plans.exec(h->inv, h->j2, nullptr);
+    h->fft2(h->inv, h->j2, false, 1, 1);
     hipLaunchKernelGGL(to_field_kernel, dim3(grid_for((size_t)(nx + 1) * (ny + 1))), dim3(256),
                        0, h->stream, h->j2, h->field, (long)(nx + 1), nx, ny,
                        1.0 / ((double)nx * ny));

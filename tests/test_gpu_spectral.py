@@ -29,7 +29,7 @@ def spec():
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("n", [64, 96, 256])
+@pytest.mark.parametrize("n", [64, 96, 256, 1024])
 def test_gpu_spectral_jacobian_vs_oracle(spec, kind, n):
     dx, dy, _, _ = vo.vm_grid(n, n)
     f = smooth_field(n, n, 6, n) + 0.01 * np.random.default_rng(n).standard_normal((n, n))
@@ -55,6 +55,25 @@ def test_gpu_spectral_vm_steps_vs_oracle(spec, kind, n, steps, dt):
     assert np.abs(ut[:n, :n] - ref).max() < 1e-10
     assert np.array_equal(ut[n, :], ut[0, :]) and np.array_equal(ut[:, n], ut[:, 0])
     assert wf[0, 0] == 0 or abs(wf[0, 0]) < 1e-9  # hybrid.jl:59 zeroes stages 1-2 only
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("n", [512, 2048])
+def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
+    """Power-of-two grids of 256..4096 run the hand-written two-pass 2-D transform
+    (fft2d_c2c.hip); CFDJ_SPEC_FFT=rocfft keeps the library plans.  Both give the same
+    fields to FFT round-off (1e-12 of max|w| after 3 steps)."""
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    out = []
+    for path in ("hand", "rocfft"):
+        monkeypatch.setenv("CFDJ_SPEC_FFT", path)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+            h.upload_interior(w0)
+            h.step(1e-3, 3)
+            out.append(h.download())
+    assert np.isfinite(out[0]).all()
+    assert np.abs(out[0] - out[1]).max() <= 1e-12 * np.abs(out[1]).max()
 
 
 @pytest.mark.parametrize("kind", KINDS)
