@@ -490,6 +490,87 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
                            it + 1 < rg.count ? item_y0(it + 1) : -1, q, tid, twL, twN);
 }
 
+// The inverse row pass of the one-GPU column-major spectrum for rows of up to 4096 reals:
+// ONE small item (XR rows: 2 at L = 2048, 256 threads) per workgroup, not persistent, the
+// LDS buffer component-wise (35 KB), 128 registers -- four workgroups per CU overlap each
+// other's loads, transforms and stores, which a single persistent workgroup with its next
+// item prefetched into registers does less well (59 -> 49 us per launch in the step at
+// 4096^2).  The c2r pre-processing of a pair (m, L - m) is formed in registers and goes
+// through the buffer one component at a time, straight into stage 0's input order.
+// CFDJ_ROWS_INV_NP=0 builds without it (the persistent kernel everywhere).  The forward
+// pass keeps the persistent 4-row items: its column-segment WRITES would shrink to 32 B
+// with 2-row items, which measured slower (85 us in the step).
+#ifndef CFDJ_ROWS_INV_NP
+#define CFDJ_ROWS_INV_NP 1
+#endif
+template <int L>
+constexpr int rows_inv_np_xr() { return 256 / Plan<L>::T > 2 ? 256 / Plan<L>::T : 2; }
+
+template <int L, int XR>
+__global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
+    const double2* __restrict__ H, double* __restrict__ f, int M,
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
+  using P = Plan<L>;
+  constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
+  __shared__ double lds[XR * P::PAD];
+  const TwGlobal<L> twL{twL_};
+  const TwGlobal<2 * L> twN{twN_};
+  const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
+  double* buf = lds + q * P::PAD;
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  const double2* base = H + (size_t)__builtin_amdgcn_readfirstlane(y0);
+  double2 o1[PAIRS], o2[PAIRS];
+  // pair i of the thread: row qq, columns m and L - m (16 consecutive lanes take 16
+  // consecutive m of one row; m = 0, with partner L/2, occurs in pair 0 only)
+  auto pair = [](int i, int& qq, int& m) {
+    const int e = threadIdx.x + i * THREADS;
+    qq = (e >> 4) % XR;
+    m = ((e >> 4) / XR) * 16 + (e & 15);
+  };
+#pragma unroll
+  for (int i = 0; i < PAIRS; ++i) {
+    int qq, m;
+    pair(i, qq, m);
+    const bool z0 = i == 0 && m == 0;
+    const double2 Xm = base[(unsigned)((size_t)m * M + qq)];
+    const double2 Xq = base[(unsigned)((size_t)(z0 ? L / 2 : L - m) * M + qq)];
+    const double2 Xp = cconj(Xq);
+    const double2 S = cadd(Xm, Xp);
+    const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
+    o1[i] = make_double2(S.x - D.y, S.y + D.x);
+    o2[i] = make_double2(S.x + D.y, D.x - S.y);
+    if (z0) {  // slot 0 = (X[0], X[L]), both real; Z[L/2] = 2 conj(X[L/2])
+      o1[i] = make_double2(Xm.x + Xm.y, Xm.x - Xm.y);
+      o2[i] = make_double2(2.0 * Xq.x, -2.0 * Xq.y);
+    }
+  }
+  double2 v[16];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      int qq, m;
+      pair(i, qq, m);
+      double* bq = lds + qq * P::PAD;
+      bq[padx(m)] = c ? o1[i].y : o1[i].x;
+      bq[padx(i == 0 && m == 0 ? L / 2 : L - m)] = c ? o2[i].y : o2[i].x;
+    }
+    __syncthreads();
+    if (c) lds_read_half<L, 0, 1>(buf, v, tid);
+    else lds_read_half<L, 0, 0>(buf, v, tid);
+  }
+  stage_regs<L, 0, 1>(v, tid, twL);
+  run_stages_half<L, 1, 1>(buf, v, tid, twL);
+  constexpr int SL = P::NSTAGES - 1;
+  constexpr int RL = P::radix(SL);
+  double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + q) * (2 * L));
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) z[out_pos<L, SL>(tid, b, r)] = v[b * RL + r];
+}
+
 // Persistent grid: `per_cu` resident workgroups per CU (LDS-limited), a multiple of 8.
 static int persistent_grid(int ncu, int per_cu, int items) {
   int nb = ncu * per_cu;
@@ -503,8 +584,21 @@ void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st);
 
 template <int L>
 void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  if (pass == 0) launch_rows_dir<L, true>(pass, a, st);
-  else launch_rows_dir<L, false>(pass, a, st);
+  if (pass == 0) {
+    launch_rows_dir<L, true>(pass, a, st);
+  } else {
+#if CFDJ_ROWS_INV_NP > 0
+    if constexpr (L <= 2048) {
+      constexpr int XR = rows_inv_np_xr<L>();
+      if (!a.tile8 && a.rows % XR == 0) {
+        hipLaunchKernelGGL((rows_inv_np_kernel<L, XR>), dim3(a.rows / XR),
+                           dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN);
+        return;
+      }
+    }
+#endif
+    launch_rows_dir<L, false>(pass, a, st);
+  }
 }
 
 template <int L, bool FWD>
