@@ -1288,7 +1288,7 @@ struct cfdj_cavity {
   double* part = nullptr;
   double* d_rms = nullptr;
   int rms_cap = 0;
-  static constexpr int kParts = 512;
+  static constexpr int kParts = 2048;  // >= the workgroups of any partial-sum producer
 
   size_t field() const { return (size_t)P * (ny + 1); }
 

@@ -212,6 +212,117 @@ __global__ __launch_bounds__(DstRowCfg<M2>::THREADS) void dst_rows_inv_kernel(
   }
 }
 
+// The inverse row pass for transforms of up to 4096 points: ONE small item (256 threads:
+// one row pair at M2 = 4096) per workgroup, not persistent, component-wise LDS (34 KB), so
+// four workgroups per CU overlap each other's loads, transforms and stores -- the shape of
+// the periodic solver's rows_inv_np_kernel.  A thread's entries all belong to one row, so
+// the real part of the packed extension (first row of a pair) is written by one half of the
+// threads and the imaginary part by the other, one component at a time.
+template <int M2>
+struct DstNpCfg {
+  static constexpr int T = Plan<M2>::T;
+  static constexpr int RP = 256 / T < 1 ? 1 : 256 / T;
+  static constexpr int ROWS = 2 * RP;
+  static constexpr int THREADS = RP * T;
+  static constexpr int ENTRIES = (M2 / 4) * ROWS / THREADS;
+};
+
+template <int M2>
+__global__ __launch_bounds__(DstNpCfg<M2>::THREADS) void dst_rows_inv_np_kernel(
+    const double2* __restrict__ T, int JT, double* __restrict__ s, int P, int ny,
+    const double2* __restrict__ tw_, const double* __restrict__ sprev,
+    double* __restrict__ part) {
+  using PL = Plan<M2>;
+  using C = DstNpCfg<M2>;
+  constexpr int nx = M2 / 2;
+  __shared__ double lds[C::RP * PL::PAD];
+  const TwGlobal<M2> tw{tw_};
+  const int q = threadIdx.x / PL::T, tid = threadIdx.x % PL::T;
+  double* buf = lds + q * PL::PAD;
+  const int slot0 = xcd_remap(blockIdx.x, gridDim.x) * C::ROWS;
+  auto entry = [](int i, int& rr, int& kap) {
+    const int e = threadIdx.x + i * C::THREADS;
+    rr = (e >> 4) % C::ROWS;
+    kap = ((e >> 4) / C::ROWS) * 16 + (e & 15);
+  };
+  double2 ent[C::ENTRIES];
+  {
+    const double2* tb = T + __builtin_amdgcn_readfirstlane(slot0);
+#pragma unroll
+    for (int i = 0; i < C::ENTRIES; ++i) {
+      int rr, kap;
+      entry(i, rr, kap);
+      ent[i] = tb[(unsigned)(kap * JT + rr)];
+    }
+  }
+  double2 v[16];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c) __syncthreads();
+    // entries -> the odd extension of their row: mode k at p = k and, negated, at
+    // p = 2nx - k; p = 0 and p = nx are zero (the kappa = 0 lanes write them)
+#pragma unroll
+    for (int i = 0; i < C::ENTRIES; ++i) {
+      int rr, kap;
+      entry(i, rr, kap);
+      if ((rr & 1) == c) {
+        double* bq = lds + (rr >> 1) * PL::PAD;
+        const int k0 = 2 * kap, k1 = k0 + 1;
+        const double v0 = k0 == 0 ? 0.0 : ent[i].x;
+        bq[padx(k0)] = v0;
+        bq[padx(k1)] = ent[i].y;
+        if (k0 != 0) bq[padx(M2 - k0)] = -v0;
+        else bq[padx(nx)] = 0.0;
+        bq[padx(M2 - k1)] = -ent[i].y;
+      }
+    }
+    __syncthreads();
+    if (c) lds_read_half<M2, 0, 1>(buf, v, tid);
+    else lds_read_half<M2, 0, 0>(buf, v, tid);
+  }
+  stage_regs<M2, 0, -1>(v, tid, tw);
+  run_stages_half<M2, 1, -1>(buf, v, tid, tw);
+  constexpr int SL = PL::NSTAGES - 1;
+  constexpr int RL = PL::radix(SL);
+  const int ja = 1 + slot0 + 2 * q;
+  const bool oka = ja <= ny - 1, okb = ja + 1 <= ny - 1;
+  double* sa = s + (size_t)ja * P;
+  double* sb = sa + P;
+  double acc = 0.0;
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) {
+      const int p = out_pos<M2, SL>(tid, b, r);
+      if (p >= 1 && p < nx) {
+        const double va = -v[b * RL + r].y, vb = v[b * RL + r].x;
+        if (oka) sa[p] = va;
+        if (okb) sb[p] = vb;
+        if (sprev != nullptr) {
+          if (oka) {
+            const double d = va - sprev[(size_t)ja * P + p];
+            acc += d * d;
+          }
+          if (okb) {
+            const double d = vb - sprev[(size_t)(ja + 1) * P + p];
+            acc += d * d;
+          }
+        }
+      }
+    }
+  if (part != nullptr) {
+    __syncthreads();  // the buffer's last readers are done
+    double* red = lds;
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = C::THREADS / 2; off > 0; off >>= 1) {
+      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  }
+}
+
 // One mode pair per workgroup: packed y-DST, times iden, packed y-DST, in place.
 #ifndef CFDJ_DST_COLS_WAVES
 #define CFDJ_DST_COLS_WAVES 3
@@ -290,16 +401,34 @@ int dst_rows_grid_t(int ny, int ncu) {
   return nb < items ? nb : items;
 }
 
+// The inverse pass's grid: one workgroup per small item where the non-persistent kernel
+// applies (transforms of up to 4096 points, CFDJ_DST_INV_NP != 0), else the persistent grid.
+#ifndef CFDJ_DST_INV_NP
+#define CFDJ_DST_INV_NP 1
+#endif
+template <int M2>
+constexpr bool dst_inv_np() { return CFDJ_DST_INV_NP != 0 && M2 <= 4096; }
+template <int M2>
+int dst_rows_inv_grid_t(int ny, int ncu) {
+  if (dst_inv_np<M2>() && ny % DstNpCfg<M2>::ROWS == 0) return ny / DstNpCfg<M2>::ROWS;
+  return dst_rows_grid_t<M2>(ny, ncu);
+}
+
 template <int M2>
 void launch_dst_rows(int pass, const DstPoissonArgs& a, hipStream_t st) {
   using C = DstRowCfg<M2>;
   const dim3 grid(dst_rows_grid_t<M2>(a.ny, a.ncu));
-  if (pass == 0)
+  if (pass == 0) {
     hipLaunchKernelGGL((dst_rows_fwd_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.w, a.P, a.ny,
                        a.T, a.JT, a.neg ? -1.0 : 1.0, a.twX);
-  else
+  } else if (dst_inv_np<M2>() && a.ny % DstNpCfg<M2>::ROWS == 0) {
+    hipLaunchKernelGGL((dst_rows_inv_np_kernel<M2>), dim3(a.ny / DstNpCfg<M2>::ROWS),
+                       dim3(DstNpCfg<M2>::THREADS), 0, st, a.T, a.JT, a.s, a.P, a.ny, a.twX,
+                       a.sprev, a.sprev ? a.part : nullptr);
+  } else {
     hipLaunchKernelGGL((dst_rows_inv_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.T, a.JT, a.s,
                        a.P, a.ny, a.twX, a.sprev, a.sprev ? a.part : nullptr);
+  }
 }
 
 template <int M2>
@@ -316,12 +445,13 @@ bool dst_poisson_supported(int nx, int ny) {
   return pow2(nx) && pow2(ny) && nx >= 512 && nx <= 4096 && ny >= 512 && ny <= 4096;
 }
 
+// Workgroups of the inverse row pass = entries of its `part` output (at most 2048).
 int dst_rows_grid(int nx, int ny, int ncu) {
   switch (2 * nx) {
-    case 1024: return dst_rows_grid_t<1024>(ny, ncu);
-    case 2048: return dst_rows_grid_t<2048>(ny, ncu);
-    case 4096: return dst_rows_grid_t<4096>(ny, ncu);
-    default: return dst_rows_grid_t<8192>(ny, ncu);
+    case 1024: return dst_rows_inv_grid_t<1024>(ny, ncu);
+    case 2048: return dst_rows_inv_grid_t<2048>(ny, ncu);
+    case 4096: return dst_rows_inv_grid_t<4096>(ny, ncu);
+    default: return dst_rows_inv_grid_t<8192>(ny, ncu);
   }
 }
 
