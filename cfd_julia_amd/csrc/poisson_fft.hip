@@ -503,10 +503,15 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 #ifndef CFDJ_ROWS_INV_NP
 #define CFDJ_ROWS_INV_NP 1
 #endif
-template <int L>
-constexpr int rows_inv_np_xr() { return 256 / Plan<L>::T > 2 ? 256 / Plan<L>::T : 2; }
+// Rows per item: 256 threads' worth, at least 2 in the column-major layout (32-B column
+// segments); in the 8-mode-tile layout of the y-slab path a single row is whole 128-B lines.
+template <int L, bool TILE>
+constexpr int rows_np_xr() {
+  constexpr int byT = 256 / Plan<L>::T;
+  return TILE ? (byT > 1 ? byT : 1) : (byT > 2 ? byT : 2);
+}
 
-template <int L, int XR>
+template <int L, int XR, bool TILE>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
@@ -518,7 +523,7 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
   const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
   double* buf = lds + q * P::PAD;
   const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
-  const double2* base = H + (size_t)__builtin_amdgcn_readfirstlane(y0);
+  const double2* base = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
   double2 o1[PAIRS], o2[PAIRS];
   // pair i of the thread: row qq, columns m and L - m (16 consecutive lanes take 16
   // consecutive m of one row; m = 0, with partner L/2, occurs in pair 0 only)
@@ -532,8 +537,8 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     int qq, m;
     pair(i, qq, m);
     const bool z0 = i == 0 && m == 0;
-    const double2 Xm = base[(unsigned)((size_t)m * M + qq)];
-    const double2 Xq = base[(unsigned)((size_t)(z0 ? L / 2 : L - m) * M + qq)];
+    const double2 Xm = base[(unsigned)sidx<TILE>(m, qq, M)];
+    const double2 Xq = base[(unsigned)sidx<TILE>(z0 ? L / 2 : L - m, qq, M)];
     const double2 Xp = cconj(Xq);
     const double2 S = cadd(Xm, Xp);
     const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
@@ -571,6 +576,86 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     for (int r = 0; r < RL; ++r) z[out_pos<L, SL>(tid, b, r)] = v[b * RL + r];
 }
 
+// The forward row pass in the same shape (one small item per workgroup, component-wise LDS,
+// four workgroups per CU), used with the 8-mode-tile layout of the y-slab path, where one
+// row's modes are whole 128-B lines; in the column-major layout a small item's column
+// segments are too short to write (see above) and the persistent kernel stays.
+template <int L, int XR, bool TILE>
+__global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
+    const double* __restrict__ f, double2* __restrict__ H, int M,
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
+  using P = Plan<L>;
+  constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
+  __shared__ double lds[XR * P::PAD];
+  const TwGlobal<L> twL{twL_};
+  const TwGlobal<2 * L> twN{twN_};
+  const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
+  double* buf = lds + q * P::PAD;
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  double2 v[16];
+  {
+    const double2* z = reinterpret_cast<const double2*>(f) + (size_t)(y0 + q) * L;
+    constexpr int R0 = P::radix(0);
+#pragma unroll
+    for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+      for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[(unsigned)in_pos<L, 0>(tid, b, r)];
+  }
+  stage_regs<L, 0, -1>(v, tid, twL);
+  run_stages_half<L, 1, -1>(buf, v, tid, twL);
+  // the transform's outputs, in natural order, through the buffer one component at a time;
+  // pair i of the thread: row qq, columns m and L - m (m = 0 pairs with L/2, pair 0 only)
+  constexpr int SL = P::NSTAGES - 1;
+  auto pair = [](int i, int& qq, int& m) {
+    const int e = threadIdx.x + i * THREADS;
+    qq = (e >> 4) % XR;
+    m = ((e >> 4) / XR) * 16 + (e & 15);
+  };
+  double2 Zm[PAIRS], Zp[PAIRS];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();
+    if (c) lds_write_half<L, SL, 1>(buf, v, tid);
+    else lds_write_half<L, SL, 0>(buf, v, tid);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      int qq, m;
+      pair(i, qq, m);
+      const double* bq = lds + qq * P::PAD;
+      const double a = bq[padx(m)], b = bq[padx(i == 0 && m == 0 ? L / 2 : L - m)];
+      if (c) {
+        Zm[i].y = a;
+        Zp[i].y = b;
+      } else {
+        Zm[i].x = a;
+        Zp[i].x = b;
+      }
+    }
+  }
+  double2* hb = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
+#pragma unroll
+  for (int i = 0; i < PAIRS; ++i) {
+    int qq, m;
+    pair(i, qq, m);
+    const bool z0 = i == 0 && m == 0;
+    const int mp = z0 ? L / 2 : L - m;
+    const double2 Zc = cconj(Zp[i]);
+    const double2 E = make_double2(0.5 * (Zm[i].x + Zc.x), 0.5 * (Zm[i].y + Zc.y));
+    const double2 D = csub(Zm[i], Zc);                      // = 2i O[m]
+    const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
+    const double2 WO = cmul(twN.w(m), O);
+    double2 o1 = cadd(E, WO);
+    double2 o2 = cconj(csub(E, WO));
+    if (z0) {  // slot 0 = X[0] + i X[L]; X[L/2] = conj(Z[L/2])
+      o1 = make_double2(Zm[i].x + Zm[i].y, Zm[i].x - Zm[i].y);
+      o2 = Zc;
+    }
+    hb[(unsigned)sidx<TILE>(m, qq, M)] = o1;
+    hb[(unsigned)sidx<TILE>(mp, qq, M)] = o2;
+  }
+}
+
 // Persistent grid: `per_cu` resident workgroups per CU (LDS-limited), a multiple of 8.
 static int persistent_grid(int ncu, int per_cu, int items) {
   int nb = ncu * per_cu;
@@ -584,21 +669,33 @@ void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st);
 
 template <int L>
 void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
-  if (pass == 0) {
-    launch_rows_dir<L, true>(pass, a, st);
-  } else {
 #if CFDJ_ROWS_INV_NP > 0
-    if constexpr (L <= 2048) {
-      constexpr int XR = rows_inv_np_xr<L>();
-      if (!a.tile8 && a.rows % XR == 0) {
-        hipLaunchKernelGGL((rows_inv_np_kernel<L, XR>), dim3(a.rows / XR),
+  // the small-item kernels: the inverse pass in both layouts, the forward pass in the
+  // 8-mode-tile layout; rows of up to 4096 (column-major) / 8192 (tiles) reals
+  if constexpr (L <= 4096) {
+    if (a.tile8) {
+      constexpr int XR = rows_np_xr<L, true>();
+      if (a.rows % XR == 0) {
+        if (pass == 0)
+          hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true>), dim3(a.rows / XR),
+                             dim3(XR * Plan<L>::T), 0, st, a.f, a.H, a.rows, a.twL, a.twN);
+        else
+          hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true>), dim3(a.rows / XR),
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN);
+        return;
+      }
+    } else if (pass != 0 && L <= 2048) {
+      constexpr int XR = rows_np_xr<L, false>();
+      if (a.rows % XR == 0) {
+        hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false>), dim3(a.rows / XR),
                            dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN);
         return;
       }
     }
-#endif
-    launch_rows_dir<L, false>(pass, a, st);
   }
+#endif
+  if (pass == 0) launch_rows_dir<L, true>(pass, a, st);
+  else launch_rows_dir<L, false>(pass, a, st);
 }
 
 template <int L, bool FWD>
