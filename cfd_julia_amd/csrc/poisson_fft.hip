@@ -302,10 +302,16 @@ __device__ __forceinline__ void cols_column(void* lds, const double2* __restrict
   double2 v[NV];
   fwd_to_inv<M>(a, v);  // v[r] = spectrum at k = tid + T*r, natural order
   const double ax = fd_symbol_x(da.aa, da.bb, da.cx[m]);
+  // From here on the thread index is an opaque copy that exists only once the forward
+  // transform is done: the loads that depend on nothing else (cos(ky) of the divide, the
+  // inverse stages' twiddles) would otherwise be hoisted to the top of the kernel and
+  // their registers stay live through the whole forward transform (170 -> 144 VGPRs).
+  int tk = tid;
+  asm volatile("" : "+v"(tk) : "v"(v[NV - 1].x));
   if constexpr (!PACKED) {
 #pragma unroll
     for (int r = 0; r < NV; ++r) {
-      const int k = tid + P::T * r;
+      const int k = tk + P::T * r;
       const double d = fd_symbol(ax, da.cc, da.cy[k]);
       const double d2 = mirror ? fd_symbol(ax, da.cc, da.cy_mirror[k]) : d;
       const double2 q = sym_apply(v[r], d, d2, sgn, mirror);
@@ -330,7 +336,7 @@ __device__ __forceinline__ void cols_column(void* lds, const double2* __restrict
     for (int r = 0; r < NV; ++r) v[r] = ocol[col_off(tid + P::T * r, da.rl_log2, da.seg)];
     __syncthreads();  // every reload precedes the final stores to the same column
   }
-  col_fft<M, 1, HALF>(lds, v, tid, twM);
+  col_fft<M, 1, HALF>(lds, v, tk, twM);
   // last inverse stage: outputs j + r*NS are in natural order -> straight to HBM
   constexpr int SL = P::NSTAGES - 1;
   constexpr int RL = P::radix(SL);
@@ -338,15 +344,18 @@ __device__ __forceinline__ void cols_column(void* lds, const double2* __restrict
   for (int b = 0; b < NV / RL; ++b)
 #pragma unroll
     for (int r = 0; r < RL; ++r)
-      ocol[col_off(out_pos<M, SL, NV>(tid, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
+      ocol[col_off(out_pos<M, SL, NV>(tk, b, r), da.rl_log2, da.seg)] = v[b * RL + r];
 }
 
 // Wavefronts per SIMD the column kernel is compiled for (its register cap): with 16 values
 // per thread one per resident workgroup when a workgroup is 4 wavefronts (M = 4096: LDS
 // allows 4, registers 3); with 8 values per thread, 4.
+#ifndef CFDJ_COLS_WAVES
+#define CFDJ_COLS_WAVES 3
+#endif
 template <int M>
 constexpr int cols_waves() {
-  return kColsNV == 8 ? 4 : (Plan<M>::T == 256 && M <= 4096 ? 3 : 2);
+  return kColsNV == 8 ? 4 : (Plan<M>::T == 256 && M <= 4096 ? CFDJ_COLS_WAVES : 2);
 }
 
 template <int M, bool MIRROR>
