@@ -43,7 +43,10 @@ __global__ __launch_bounds__(Plan<N>::T) void c2c_rows_kernel(double2* __restric
     for (int r = 0; r < RL; ++r) row[out_pos<N, SL>(tid, b, r)] = v[b * RL + r];
 }
 
-constexpr int kColsPerGroup = 4;
+#ifndef CFDJ_C2C_XC
+#define CFDJ_C2C_XC 4
+#endif
+constexpr int kColsPerGroup = CFDJ_C2C_XC;
 
 template <int M, int DIR>
 __global__ __launch_bounds__(kColsPerGroup* Plan<M>::T) void c2c_cols_kernel(
