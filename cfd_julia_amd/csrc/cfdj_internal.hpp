@@ -195,6 +195,14 @@ void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
 bool c2c2d_supported(int nx, int ny);
 void launch_c2c2d(double2* a, int nx, int ny, int batch, int dir, const double2* twX,
                   const double2* twY, hipStream_t st);
+// real(ifft2(a)) (unnormalised) -> r, `a` overwritten; fft2(complex(r, 0)) -> a.
+void launch_c2r2d(double2* a, double* r, int nx, int ny, int batch, const double2* twX,
+                  const double2* twY, hipStream_t st);
+void launch_r2c2d(const double* r, double2* a, int nx, int ny, int batch, const double2* twX,
+                  const double2* twY, hipStream_t st);
+// r[0] = real(ifft2(wf)), r[1] = real(ifft2(wf / (kx[i]^2 + kx[j]^2))), x = 2 scratch arrays.
+void launch_hybrid_c2r2d(const double2* wf, const double* kx, double2* x, double* r, int nx,
+                         int ny, const double2* twX, const double2* twY, hipStream_t st);
 
 // Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row

@@ -90,6 +90,32 @@ __global__ void hybrid_jac_kernel(const double2* __restrict__ X, double2* __rest
   }
 }
 
+// The same on real fields (w = Rw / N, s = Rs / N), real result: the hand-written
+// transforms hand over real(ifft(.)) as real arrays and take the product as one.
+__global__ void hybrid_jac_real_kernel(const double* __restrict__ Rw,
+                                       const double* __restrict__ Rs, double* __restrict__ Rj,
+                                       int nx, int ny, double inv_n, double gg, double hh) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const int ie = i + 1 == nx ? 0 : i + 1, iw = i == 0 ? nx - 1 : i - 1;
+    const int jn = j + 1 == ny ? 0 : j + 1, js = j == 0 ? ny - 1 : j - 1;
+    auto W = [&](int a, int b) { return Rw[(size_t)b * nx + a] * inv_n; };
+    auto P = [&](int a, int b) { return Rs[(size_t)b * nx + a] * inv_n; };
+    const double wE = W(ie, j), wW = W(iw, j), wN = W(i, jn), wS = W(i, js);
+    const double wNE = W(ie, jn), wSW = W(iw, js), wNW = W(iw, jn), wSE = W(ie, js);
+    const double sE = P(ie, j), sW = P(iw, j), sN = P(i, jn), sS = P(i, js);
+    const double sNE = P(ie, jn), sSW = P(iw, js), sNW = P(iw, jn), sSE = P(ie, js);
+    const double j1 = gg * ((wE - wW) * (sN - sS) - (wN - wS) * (sE - sW));
+    const double j2 =
+        gg * (wE * (sNE - sSE) - wW * (sNW - sSW) - wN * (sNE - sNW) + wS * (sSE - sSW));
+    const double j3 =
+        gg * (wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS));
+    Rj[t] = -(j1 + j2 + j3) * hh;
+  }
+}
+
 // pseudospectral_*.jl:109-122 derivatives of w_f, placed on the px x py product grid:
 //   2/3 rule (px = nx): modes i in [nxe/2, nx - nxe/2) or j in [nye/2, ny - nye/2) zeroed
 //           (pseudospectral_23_rule.jl:124-133, 0-based);
@@ -145,6 +171,17 @@ __global__ void ps_product_kernel(const double2* __restrict__ D, double2* __rest
     const double j1 = D[t].x * inv_np, j2 = D[np + t].x * inv_np;
     const double j3 = D[2 * np + t].x * inv_np, j4 = D[3 * np + t].x * inv_np;
     J[t] = make_double2(j1 * j2 - j3 * j4, 0.0);
+  }
+}
+
+// ... on real fields (the four real(ifft(.)) as real arrays), real product.
+__global__ void ps_product_real_kernel(const double* __restrict__ D, double* __restrict__ Rj,
+                                       size_t np, double inv_np) {
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < np;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const double j1 = D[t] * inv_np, j2 = D[np + t] * inv_np;
+    const double j3 = D[2 * np + t] * inv_np, j4 = D[3 * np + t] * inv_np;
+    Rj[t] = j1 * j2 - j3 * j4;
   }
 }
 
@@ -237,6 +274,10 @@ struct cfdj_spec {
   bool hand_n = false, hand_p = false;           // nx x ny / px x py
   double2 *tw_n = nullptr, *tw_p = nullptr;      // twiddle tables (nx == ny, px == py)
   int nb = 2;                                    // arrays in X
+  // physical-space fields of the hand-written path: nb real(ifft(.)) arrays and the
+  // real product (real_fields: CFDJ_SPEC_REAL=0 keeps them complex)
+  double *R = nullptr, *Rj = nullptr;
+  bool real_fields = false;
 
   // In-place 2-D transform of `batch` arrays: the library plan `pl` or the hand-written one.
   void fft2(rocfft_plan pl, double2* buf, bool product_grid, int batch, int dir) {
@@ -257,11 +298,19 @@ struct cfdj_spec {
   void jacobian(const double2* wf, double2* jf) {
     const unsigned gb = grid_for(np());
     if (kind == CFDJ_SPEC_HYBRID) {
+      const double gg = 1.0 / (4.0 * dx * dy), hh = 1.0 / 3.0;
+      if (real_fields) {  // w_f and w_f / k2 are formed inside the inverse column pass
+        launch_hybrid_c2r2d(wf, kx, X, R, nx, ny, tw_n, tw_n, stream);
+        hipLaunchKernelGGL(hybrid_jac_real_kernel, dim3(grid_for(n())), dim3(256), 0, stream, R,
+                           R + n(), Rj, nx, ny, 1.0 / ((double)nx * ny), gg, hh);
+        CFDJ_HIP(hipGetLastError());
+        launch_r2c2d(Rj, jf, nx, ny, 1, tw_n, tw_n, stream);
+        return;
+      }
       hipLaunchKernelGGL(hybrid_prep_kernel, dim3(grid_for(n())), dim3(256), 0, stream, wf, kx,
                          X, nx, ny);
       CFDJ_HIP(hipGetLastError());
       fft2(inv_b, X, true, nb, 1);
-      const double gg = 1.0 / (4.0 * dx * dy), hh = 1.0 / 3.0;
       hipLaunchKernelGGL(hybrid_jac_kernel, dim3(grid_for(n())), dim3(256), 0, stream, X, jf,
                          nx, ny, 1.0 / ((double)nx * ny), gg, hh);
       CFDJ_HIP(hipGetLastError());
@@ -275,6 +324,14 @@ struct cfdj_spec {
     hipLaunchKernelGGL(ps_derivs_kernel, dim3(gb), dim3(256), 0, stream, wf, kx, X, nx, ny, px,
                        py, r32 ? 1 : 0, tx0, tx1, ty0, ty1, sc, sd);
     CFDJ_HIP(hipGetLastError());
+    if (real_fields && !r32) {  // 2/3 rule on a power-of-two grid: product grid = grid
+      launch_c2r2d(X, R, nx, ny, nb, tw_n, tw_n, stream);
+      hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
+                         1.0 / sc);
+      CFDJ_HIP(hipGetLastError());
+      launch_r2c2d(Rj, jf, nx, ny, 1, tw_n, tw_n, stream);
+      return;
+    }
     fft2(inv_b, X, true, nb, 1);
     double2* P = r32 ? J : jf;
     hipLaunchKernelGGL(ps_product_kernel, dim3(gb), dim3(256), 0, stream, X, P, np(),
@@ -315,6 +372,8 @@ struct cfdj_spec {
     if (tw_p != tw_n) dfree(tw_p);
     dfree(tw_n);
     for (double2** p : {&wn, &w1, &w2, &jn, &j1, &j2, &X, &J}) dfree(*p);
+    dfree(R);
+    dfree(Rj);
     dfree(kx);
     dfree(field);
     if (stream) (void)hipStreamDestroy(stream);
@@ -370,6 +429,12 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     h->hand_p = want_hand && c2c2d_supported(h->px, h->py);
     if (h->hand_n) h->tw_n = twiddle_table(nx);
     if (h->hand_p) h->tw_p = (h->px == nx && h->tw_n) ? h->tw_n : twiddle_table(h->px);
+    const char* re_ = std::getenv("CFDJ_SPEC_REAL");
+    h->real_fields = h->hand_n && h->px == nx && !(re_ && re_[0] == '0');
+    if (h->real_fields) {
+      h->R = dalloc<double>((size_t)nb * n);
+      h->Rj = dalloc<double>(n);
+    }
     h->X = dalloc<double2>((size_t)nb * np);
     if (kind == CFDJ_SPEC_PS32) h->J = dalloc<double2>(np);
     h->field = dalloc<double>((size_t)(nx + 1) * (ny + 1));

@@ -61,19 +61,26 @@ def test_gpu_spectral_vm_steps_vs_oracle(spec, kind, n, steps, dt):
 @pytest.mark.parametrize("n", [512, 2048])
 def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
     """Power-of-two grids of 256..4096 run the hand-written two-pass 2-D transform
-    (fft2d_c2c.hip); CFDJ_SPEC_FFT=rocfft keeps the library plans.  Both give the same
-    fields to FFT round-off (1e-12 of max|w| after 3 steps)."""
+    (fft2d_c2c.hip) with real physical-space fields; CFDJ_SPEC_REAL=0 keeps those fields
+    complex, CFDJ_SPEC_FFT=rocfft keeps the library plans.  All give the same fields to FFT
+    round-off (1e-12 of max|w| after 3 steps); real and complex fields the same bits."""
     dx, dy, x, y = vo.vm_grid(n, n)
     w0 = vo.vm_ic(n, n, x, y)
-    out = []
-    for path in ("hand", "rocfft"):
-        monkeypatch.setenv("CFDJ_SPEC_FFT", path)
+    out = {}
+    for name, env in (("real", {}), ("complex", {"CFDJ_SPEC_REAL": "0"}),
+                      ("rocfft", {"CFDJ_SPEC_FFT": "rocfft"})):
+        for k in ("CFDJ_SPEC_REAL", "CFDJ_SPEC_FFT"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
         with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
             h.upload_interior(w0)
             h.step(1e-3, 3)
-            out.append(h.download())
-    assert np.isfinite(out[0]).all()
-    assert np.abs(out[0] - out[1]).max() <= 1e-12 * np.abs(out[1]).max()
+            out[name] = h.download()
+    assert np.isfinite(out["real"]).all()
+    scale = np.abs(out["rocfft"]).max()
+    assert np.abs(out["real"] - out["rocfft"]).max() <= 1e-12 * scale
+    assert np.abs(out["complex"] - out["rocfft"]).max() <= 1e-12 * scale
 
 
 @pytest.mark.parametrize("kind", KINDS)
