@@ -204,6 +204,32 @@ void launch_r2c2d(const double* r, double2* a, int nx, int ny, int batch, const 
 void launch_hybrid_c2r2d(const double2* wf, const double* kx, double2* x, double* r, int nx,
                          int ny, const double2* twX, const double2* twY, hipStream_t st);
 
+// 2-D transforms of REAL n-by-n fields on the half spectrum (fft2d_r2c.hip): modes kx index
+// m = 0..n/2, all ky; element (m, k) at m n + k (ky contiguous), column n/2 = the kx Nyquist
+// column.  Unnormalised both ways.
+struct HalfSpecArgs {
+  int n;                // nx = ny
+  const double2* twL;   // exp(-2 pi i k/(n/2))
+  const double2* twN;   // exp(-2 pi i k/n)
+  int ncu;              // compute units (persistent row pass)
+  const double* kx;     // wavenumbers (Common.jl:190-199), n entries; ky = kx
+  int tx0, ty0, ty1;    // 2/3 rule: indices tx0 <= i < n - tx0, ty0 <= k < ty1 are zeroed
+};
+// Inverse modes: which arrays the column pass forms from the one spectrum w_f it reads.
+//   kHalfPlain  1 array : w_f
+//   kHalfHybrid 2 arrays: w_f, w_f / k2                          (hybrid.jl:103,115)
+//   kHalfPs23   4 arrays: i kx w_f / k2, i ky w_f, i ky w_f / k2, i kx w_f, 2/3-rule modes
+//                         zeroed                      (pseudospectral_23_rule.jl:109-133)
+enum { kHalfPlain = 1, kHalfHybrid = 2, kHalfPs23 = 3 };
+bool half2d_supported(int nx, int ny);
+// hs = fft2(r) (half); scratch: n/2 x n complex.
+void launch_half_r2c2d(const HalfSpecArgs& a, const double* r, double2* scratch, double2* hs,
+                       hipStream_t st);
+// r[b] = real(ifft2(factor_b(hs))) n n, b < arrays of `mode`; x: arrays x (n/2 x n) complex
+// scratch.  hs is left intact.
+void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, double2* x, double* r,
+                       hipStream_t st);
+
 // Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row
 // per rank (row 0 of each slab); interior blocks by DST-I (odd-extension FFT of length

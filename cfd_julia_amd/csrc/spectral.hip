@@ -203,15 +203,16 @@ __global__ void ps_unpad_kernel(const double2* __restrict__ Jp, double2* __restr
 // hybrid.jl:44-67, one RK3 / Crank-Nicolson substep.  z = .5dt k2 / re, d = alpha z;
 // out = ((1 - d)/(1 + d)) * w + (cA * jA + cB * jB) / (1 + d)   (stage 1: cB = 0, no jB);
 // out[1,1] = 0 after stages 1 and 2.
-template <int STAGE>
+// HALF: the arrays are half spectra ((nx/2 + 1) columns of ny, ky contiguous).
+template <int STAGE, bool HALF>
 __global__ void cn_update_kernel(const double2* __restrict__ w, const double2* __restrict__ jA,
                                  const double2* __restrict__ jB, double2* __restrict__ out,
                                  const double* __restrict__ kx, int nx, int ny, double hdt,
                                  double re, double alpha, double cA, double cB) {
-  const size_t n = (size_t)nx * ny;
+  const size_t n = HALF ? (size_t)(nx / 2 + 1) * ny : (size_t)nx * ny;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
        t += (size_t)gridDim.x * blockDim.x) {
-    const int i = (int)(t % nx), j = (int)(t / nx);
+    const int i = HALF ? (int)(t / ny) : (int)(t % nx), j = HALF ? (int)(t % ny) : (int)(t / nx);
     const double k2 = kx[i] * kx[i] + kx[j] * kx[j];
     const double z = hdt * k2 / re;
     const double d = alpha * z;
@@ -239,6 +240,44 @@ __global__ void to_field_kernel(const double2* __restrict__ X, double* __restric
     const int i = (int)(t % (nx + 1)), j = (int)(t / (nx + 1));
     const int a = i == nx ? 0 : i, b = j == ny ? 0 : j;
     ut[(size_t)j * ldu + i] = X[(size_t)b * nx + a].x * inv_n;
+  }
+}
+
+// ... from a real nx x ny array R = real(ifft(.)) * (nx ny).
+__global__ void to_field_real_kernel(const double* __restrict__ R, double* __restrict__ ut,
+                                     long ldu, int nx, int ny, double inv_n) {
+  const size_t n = (size_t)(nx + 1) * (ny + 1);
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % (nx + 1)), j = (int)(t / (nx + 1));
+    const int a = i == nx ? 0 : i, b = j == ny ? 0 : j;
+    ut[(size_t)j * ldu + i] = R[(size_t)b * nx + a] * inv_n;
+  }
+}
+
+// Full spectrum (nx x ny, kx contiguous) <-> half spectrum ((nx/2 + 1) columns of ny, ky
+// contiguous) of a real field: the other half is conj(w_f(-kx, -ky)).
+__global__ void full_to_half_kernel(const double2* __restrict__ full, double2* __restrict__ hs,
+                                    int nx, int ny) {
+  const size_t n = (size_t)(nx / 2 + 1) * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int m = (int)(t / ny), k = (int)(t % ny);
+    hs[t] = full[(size_t)k * nx + m];
+  }
+}
+__global__ void half_to_full_kernel(const double2* __restrict__ hs, double2* __restrict__ full,
+                                    int nx, int ny) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    if (i <= nx / 2) {
+      full[t] = hs[(size_t)i * ny + j];
+    } else {
+      const double2 v = hs[(size_t)(nx - i) * ny + (j == 0 ? 0 : ny - j)];
+      full[t] = make_double2(v.x, -v.y);
+    }
   }
 }
 
@@ -278,6 +317,13 @@ struct cfdj_spec {
   // real product (real_fields: CFDJ_SPEC_REAL=0 keeps them complex)
   double *R = nullptr, *Rj = nullptr;
   bool real_fields = false;
+  // half-spectrum state (fft2d_r2c.hip; square power-of-two grids of 1024..4096, hybrid and
+  // 2/3 rule): every spectrum above holds the modes kx index 0..nx/2 only, ky contiguous;
+  // the C interface converts (CFDJ_SPEC_HALF=0 keeps the full spectra)
+  bool half = false;
+  Fused fz;
+  HalfSpecArgs ha{};
+  size_t nh() const { return (size_t)(nx / 2 + 1) * ny; }
 
   // In-place 2-D transform of `batch` arrays: the library plan `pl` or the hand-written one.
   void fft2(rocfft_plan pl, double2* buf, bool product_grid, int batch, int dir) {
@@ -297,6 +343,23 @@ struct cfdj_spec {
   // jf = fft(-J(w, psi)) of the spectrum wf (hybrid.jl:92-152 / pseudospectral_*.jl).
   void jacobian(const double2* wf, double2* jf) {
     const unsigned gb = grid_for(np());
+    if (half) {
+      // both inverse transforms' inputs are formed inside their column pass; X is the
+      // column-pass scratch of both directions
+      if (kind == CFDJ_SPEC_HYBRID) {
+        launch_half_c2r2d(ha, kHalfHybrid, wf, X, R, stream);
+        hipLaunchKernelGGL(hybrid_jac_real_kernel, dim3(grid_for(n())), dim3(256), 0, stream, R,
+                           R + n(), Rj, nx, ny, 1.0 / ((double)nx * ny), 1.0 / (4.0 * dx * dy),
+                           1.0 / 3.0);
+      } else {
+        launch_half_c2r2d(ha, kHalfPs23, wf, X, R, stream);
+        hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
+                           1.0 / ((double)px * py));
+      }
+      CFDJ_HIP(hipGetLastError());
+      launch_half_r2c2d(ha, Rj, X, jf, stream);
+      return;
+    }
     if (kind == CFDJ_SPEC_HYBRID) {
       const double gg = 1.0 / (4.0 * dx * dy), hh = 1.0 / 3.0;
       if (real_fields) {  // w_f and w_f / k2 are formed inside the inverse column pass
@@ -348,9 +411,33 @@ struct cfdj_spec {
   template <int STAGE>
   void update(const double2* w, const double2* jA, const double2* jB, double2* out, double dt,
               double alpha, double cA, double cB) {
-    hipLaunchKernelGGL(cn_update_kernel<STAGE>, dim3(grid_for(n())), dim3(256), 0, stream, w,
-                       jA, jB, out, kx, nx, ny, 0.5 * dt, re, alpha, cA, cB);
+    if (half)
+      hipLaunchKernelGGL((cn_update_kernel<STAGE, true>), dim3(grid_for(nh())), dim3(256), 0,
+                         stream, w, jA, jB, out, kx, nx, ny, 0.5 * dt, re, alpha, cA, cB);
+    else
+      hipLaunchKernelGGL((cn_update_kernel<STAGE, false>), dim3(grid_for(n())), dim3(256), 0,
+                         stream, w, jA, jB, out, kx, nx, ny, 0.5 * dt, re, alpha, cA, cB);
     CFDJ_HIP(hipGetLastError());
+  }
+
+  // Full spectrum in `full` (device) -> the state layout in `dst`, and back.
+  void import_spectrum(const double2* full, double2* dst) {
+    if (half) {
+      hipLaunchKernelGGL(full_to_half_kernel, dim3(grid_for(nh())), dim3(256), 0, stream, full,
+                         dst, nx, ny);
+      CFDJ_HIP(hipGetLastError());
+    } else {
+      CFDJ_HIP(hipMemcpyAsync(dst, full, n() * sizeof(double2), hipMemcpyDeviceToDevice, stream));
+    }
+  }
+  void export_spectrum(const double2* src, double2* full) {
+    if (half) {
+      hipLaunchKernelGGL(half_to_full_kernel, dim3(grid_for(n())), dim3(256), 0, stream, src,
+                         full, nx, ny);
+      CFDJ_HIP(hipGetLastError());
+    } else {
+      CFDJ_HIP(hipMemcpyAsync(full, src, n() * sizeof(double2), hipMemcpyDeviceToDevice, stream));
+    }
   }
 
   // hybrid.jl:41-67 (alpha, gamma, rho of hybrid.jl:30-32)
@@ -374,6 +461,7 @@ struct cfdj_spec {
     for (double2** p : {&wn, &w1, &w2, &jn, &j1, &j2, &X, &J}) dfree(*p);
     dfree(R);
     dfree(Rj);
+    fz.destroy();
     dfree(kx);
     dfree(field);
     if (stream) (void)hipStreamDestroy(stream);
@@ -431,6 +519,14 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     if (h->hand_p) h->tw_p = (h->px == nx && h->tw_n) ? h->tw_n : twiddle_table(h->px);
     const char* re_ = std::getenv("CFDJ_SPEC_REAL");
     h->real_fields = h->hand_n && h->px == nx && !(re_ && re_[0] == '0');
+    const char* he = std::getenv("CFDJ_SPEC_HALF");
+    h->half = h->real_fields && half2d_supported(nx, ny) && !(he && he[0] == '0');
+    if (h->half) {
+      h->fz.init(nx, ny);
+      const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
+      h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,
+                           ny - nye / 2};
+    }
     if (h->real_fields) {
       h->R = dalloc<double>((size_t)nb * n);
       h->Rj = dalloc<double>(n);
@@ -464,10 +560,16 @@ int cfdj_spec_upload(cfdj_spec* h, const double* wn, long ldw) {
     CFDJ_HIP(hipMemcpy2DAsync(h->field, (nx + 1) * sizeof(double), wn + 1 + ldw,
                               ldw * sizeof(double), nx * sizeof(double), ny,
                               hipMemcpyHostToDevice, h->stream));
-    hipLaunchKernelGGL(to_complex_kernel, dim3(grid_for(h->n())), dim3(256), 0, h->stream,
-                       h->field, (long)(nx + 1), h->wn, nx, ny);
-    CFDJ_HIP(hipGetLastError());
-    h->fft2(h->fwd, h->wn, false, 1, -1);
+    if (h->half) {
+      CFDJ_HIP(hipMemcpy2DAsync(h->Rj, nx * sizeof(double), h->field, (nx + 1) * sizeof(double),
+                                nx * sizeof(double), ny, hipMemcpyDeviceToDevice, h->stream));
+      launch_half_r2c2d(h->ha, h->Rj, h->X, h->wn, h->stream);
+    } else {
+      hipLaunchKernelGGL(to_complex_kernel, dim3(grid_for(h->n())), dim3(256), 0, h->stream,
+                         h->field, (long)(nx + 1), h->wn, nx, ny);
+      CFDJ_HIP(hipGetLastError());
+      h->fft2(h->fwd, h->wn, false, 1, -1);
+    }
     CFDJ_HIP(hipMemsetAsync(h->wn, 0, sizeof(double2), h->stream));
     CFDJ_HIP(hipStreamSynchronize(h->stream));
   });
@@ -490,12 +592,18 @@ int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu) {
     CFDJ_REQUIRE(ldu >= (long)h->nx + 1, "ldu: leading dimension too small");
     select_device(h->device);
     const int nx = h->nx, ny = h->ny;
-    CFDJ_HIP(hipMemcpyAsync(h->j2, h->wn, h->n() * sizeof(double2), hipMemcpyDeviceToDevice,
-                            h->stream));  // j2 is scratch between steps
-    h->fft2(h->inv, h->j2, false, 1, 1);
-    hipLaunchKernelGGL(to_field_kernel, dim3(grid_for((size_t)(nx + 1) * (ny + 1))), dim3(256),
-                       0, h->stream, h->j2, h->field, (long)(nx + 1), nx, ny,
-                       1.0 / ((double)nx * ny));
+    const unsigned gf = grid_for((size_t)(nx + 1) * (ny + 1));
+    if (h->half) {
+      launch_half_c2r2d(h->ha, kHalfPlain, h->wn, h->X, h->R, h->stream);
+      hipLaunchKernelGGL(to_field_real_kernel, dim3(gf), dim3(256), 0, h->stream, h->R,
+                         h->field, (long)(nx + 1), nx, ny, 1.0 / ((double)nx * ny));
+    } else {
+      CFDJ_HIP(hipMemcpyAsync(h->j2, h->wn, h->n() * sizeof(double2), hipMemcpyDeviceToDevice,
+                              h->stream));  // j2 is scratch between steps
+      h->fft2(h->inv, h->j2, false, 1, 1);
+      hipLaunchKernelGGL(to_field_kernel, dim3(gf), dim3(256), 0, h->stream, h->j2, h->field,
+                         (long)(nx + 1), nx, ny, 1.0 / ((double)nx * ny));
+    }
     CFDJ_HIP(hipGetLastError());
     CFDJ_HIP(hipMemcpy2DAsync(ut, ldu * sizeof(double), h->field, (nx + 1) * sizeof(double),
                               (nx + 1) * sizeof(double), ny + 1, hipMemcpyDeviceToHost,
@@ -509,7 +617,8 @@ int cfdj_spec_get_spectrum(cfdj_spec* h, double* wf) {
   return guard([&] {
     CFDJ_REQUIRE(h && wf, "NULL argument");
     select_device(h->device);
-    CFDJ_HIP(hipMemcpyAsync(wf, h->wn, h->n() * sizeof(double2), hipMemcpyDeviceToHost,
+    h->export_spectrum(h->wn, h->j2);  // j2 is scratch between steps
+    CFDJ_HIP(hipMemcpyAsync(wf, h->j2, h->n() * sizeof(double2), hipMemcpyDeviceToHost,
                             h->stream));
     CFDJ_HIP(hipStreamSynchronize(h->stream));
   });
@@ -519,8 +628,9 @@ int cfdj_spec_set_spectrum(cfdj_spec* h, const double* wf) {
   return guard([&] {
     CFDJ_REQUIRE(h && wf, "NULL argument");
     select_device(h->device);
-    CFDJ_HIP(hipMemcpyAsync(h->wn, wf, h->n() * sizeof(double2), hipMemcpyHostToDevice,
+    CFDJ_HIP(hipMemcpyAsync(h->j2, wf, h->n() * sizeof(double2), hipMemcpyHostToDevice,
                             h->stream));
+    h->import_spectrum(h->j2, h->wn);
     CFDJ_HIP(hipStreamSynchronize(h->stream));
   });
 }
@@ -531,8 +641,10 @@ int cfdj_spec_jacobian(cfdj_spec* h, const double* wf, double* jf) {
     CFDJ_REQUIRE(h && wf && jf, "NULL argument");
     select_device(h->device);
     const size_t b = h->n() * sizeof(double2);
-    CFDJ_HIP(hipMemcpyAsync(h->w2, wf, b, hipMemcpyHostToDevice, h->stream));
-    h->jacobian(h->w2, h->j2);
+    CFDJ_HIP(hipMemcpyAsync(h->j2, wf, b, hipMemcpyHostToDevice, h->stream));
+    h->import_spectrum(h->j2, h->w2);
+    h->jacobian(h->w2, h->j1);
+    h->export_spectrum(h->j1, h->j2);
     CFDJ_HIP(hipMemcpyAsync(jf, h->j2, b, hipMemcpyDeviceToHost, h->stream));
     CFDJ_HIP(hipStreamSynchronize(h->stream));
   });

@@ -60,16 +60,19 @@ def test_gpu_spectral_vm_steps_vs_oracle(spec, kind, n, steps, dt):
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("n", [512, 2048])
 def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
-    """Power-of-two grids of 256..4096 run the hand-written two-pass 2-D transform
-    (fft2d_c2c.hip) with real physical-space fields; CFDJ_SPEC_REAL=0 keeps those fields
-    complex, CFDJ_SPEC_FFT=rocfft keeps the library plans.  All give the same fields to FFT
-    round-off (1e-12 of max|w| after 3 steps); real and complex fields the same bits."""
+    """Power-of-two grids run hand-written transforms: from 1024 on (hybrid, 2/3 rule) the
+    real transforms on the half spectrum (fft2d_r2c.hip), below that -- or with
+    CFDJ_SPEC_HALF=0 -- the two-pass complex transform (fft2d_c2c.hip) with real
+    physical-space fields; CFDJ_SPEC_REAL=0 keeps those fields complex, CFDJ_SPEC_FFT=rocfft
+    keeps the library plans.  All give the same fields to FFT round-off (1e-12 of max|w| after
+    3 steps) and the same full spectrum through the C interface."""
     dx, dy, x, y = vo.vm_grid(n, n)
     w0 = vo.vm_ic(n, n, x, y)
-    out = {}
-    for name, env in (("real", {}), ("complex", {"CFDJ_SPEC_REAL": "0"}),
-                      ("rocfft", {"CFDJ_SPEC_FFT": "rocfft"})):
-        for k in ("CFDJ_SPEC_REAL", "CFDJ_SPEC_FFT"):
+    out, spc = {}, {}
+    envs = ("CFDJ_SPEC_HALF", "CFDJ_SPEC_REAL", "CFDJ_SPEC_FFT")
+    for name, env in (("half", {}), ("real", {"CFDJ_SPEC_HALF": "0"}),
+                      ("complex", {"CFDJ_SPEC_REAL": "0"}), ("rocfft", {"CFDJ_SPEC_FFT": "rocfft"})):
+        for k in envs:
             monkeypatch.delenv(k, raising=False)
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -77,10 +80,30 @@ def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
             h.upload_interior(w0)
             h.step(1e-3, 3)
             out[name] = h.download()
-    assert np.isfinite(out["real"]).all()
+            spc[name] = h.spectrum()
     scale = np.abs(out["rocfft"]).max()
-    assert np.abs(out["real"] - out["rocfft"]).max() <= 1e-12 * scale
-    assert np.abs(out["complex"] - out["rocfft"]).max() <= 1e-12 * scale
+    sscale = np.abs(spc["rocfft"]).max()
+    for name in ("half", "real", "complex"):
+        assert np.isfinite(out[name]).all()
+        assert np.abs(out[name] - out["rocfft"]).max() <= 1e-12 * scale, name
+        assert np.abs(spc[name] - spc["rocfft"]).max() <= 1e-12 * sscale, name
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+def test_gpu_spectral_half_spectrum_round_trip(spec, kind):
+    """set_spectrum / spectrum through the half-spectrum state (n = 1024): the full spectrum
+    of a real field comes back bit for bit, its Nyquist row and column included."""
+    n = 1024
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    f = smooth_field(n, n, 5, n) + 0.01 * np.random.default_rng(7).standard_normal((n, n))
+    wf = so.to_spectral(f)
+    with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+        h.set_spectrum(wf)
+        back = h.spectrum()
+    i = np.arange(n // 2 + 1)
+    assert np.array_equal(back[i, :], wf[i, :])
+    mirror = np.conj(wf[(-np.arange(n)) % n][:, (-np.arange(n)) % n])
+    assert np.array_equal(back[n // 2 + 1:, :], mirror[n // 2 + 1:, :])
 
 
 @pytest.mark.parametrize("kind", KINDS)

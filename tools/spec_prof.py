@@ -1,5 +1,5 @@
 import math, sys, os
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np
 from cfd_julia_amd.spectral import SpectralNS2D
 from cfd_julia_amd.common import vm_ic
