@@ -64,6 +64,18 @@ __device__ __forceinline__ double2 half_factor(double2 w, int arr, int m, int k,
   }
 }
 
+// The scratch spectrum between the column and the row pass: column-major (m M + y), or in
+// the row passes' 8-mode tiles (((m/8) M + y) 8 + m%8) where a row's modes are whole lines.
+#ifndef CFDJ_HALF_TILE8
+#define CFDJ_HALF_TILE8 0
+#endif
+constexpr bool kTile8 = CFDJ_HALF_TILE8 != 0;
+template <int M>
+__device__ __forceinline__ size_t xidx(int m, int y) {
+  if constexpr (kTile8) return ((((size_t)(m >> 3)) * M + y) << 3) + (m & 7);
+  else return (size_t)m * M + y;
+}
+
 // (c[k] + conj c[-k]) / 2
 __device__ __forceinline__ double2 herm_part(double2 ck, double2 cq) {
   return make_double2(0.5 * (ck.x + cq.x), 0.5 * (ck.y - cq.y));
@@ -89,7 +101,7 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
     for (int r = 0; r < R0; ++r) {
       const int k = in_pos<M, 0>(tid, b, r);
       if constexpr (MODE == 0) {
-        v[b * R0 + r] = col[k];
+        v[b * R0 + r] = src[xidx<M>(m, k)];
       } else if constexpr (!EDGE) {
         v[b * R0 + r] = half_factor<MODE>(col[k], arr, m, k, a);
       } else {
@@ -110,7 +122,10 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
 #pragma unroll
   for (int b = 0; b < 16 / RL; ++b)
 #pragma unroll
-    for (int r = 0; r < RL; ++r) ocol[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
+    for (int r = 0; r < RL; ++r) {
+      if constexpr (MODE == 0) ocol[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
+      else dst[xidx<M>(m, out_pos<M, SL>(tid, b, r))] = v[b * RL + r];
+    }
   if constexpr (MODE == 0 && EDGE) {
     // Z = FFT_y(X0 + i XL), X0 and XL real: F0[k] = (Z[k] + conj Z[-k]) / 2,
     // FL[k] = (Z[k] - conj Z[-k]) / (2i); a thread owns the pair (k, M - k)
@@ -149,8 +164,7 @@ __global__ __launch_bounds__(Plan<M>::T) void half_cols_kernel(const HalfSpecArg
   if constexpr (MODE == kHalfPs23) {
     // columns the 2/3 rule zeroes on both sides (+m and -m): no transform
     if (m > a.tx0) {
-      double2* ocol = out + (size_t)m * M;
-      for (int k = tid; k < M; k += P::T) ocol[k] = make_double2(0.0, 0.0);
+      for (int k = tid; k < M; k += P::T) out[xidx<M>(m, k)] = make_double2(0.0, 0.0);
       return;
     }
   }
@@ -196,6 +210,7 @@ FusedPoissonArgs row_args(const HalfSpecArgs& a, const double* f, double* s, dou
   p.f = f;
   p.s = s;
   p.H = p.C = H;
+  p.tile8 = kTile8 ? 1 : 0;
   p.twL = a.twL;
   p.twN = a.twN;
   p.ncu = a.ncu;

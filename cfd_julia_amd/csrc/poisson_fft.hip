@@ -514,10 +514,13 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 #endif
 // Rows per item: 256 threads' worth, at least 2 in the column-major layout (32-B column
 // segments); in the 8-mode-tile layout of the y-slab path a single row is whole 128-B lines.
+#ifndef CFDJ_ROWS_NP_XR_MIN
+#define CFDJ_ROWS_NP_XR_MIN 2
+#endif
 template <int L, bool TILE>
 constexpr int rows_np_xr() {
   constexpr int byT = 256 / Plan<L>::T;
-  return TILE ? (byT > 1 ? byT : 1) : (byT > 2 ? byT : 2);
+  return TILE ? (byT > 1 ? byT : 1) : (byT > CFDJ_ROWS_NP_XR_MIN ? byT : CFDJ_ROWS_NP_XR_MIN);
 }
 
 template <int L, int XR, bool TILE>

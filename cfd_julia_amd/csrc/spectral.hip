@@ -23,6 +23,7 @@
 #include <memory>
 
 #include "host_common.hpp"
+#include "stencil.hpp"
 
 namespace cfdj {
 
@@ -113,6 +114,106 @@ __global__ void hybrid_jac_real_kernel(const double* __restrict__ Rw,
     const double j3 =
         gg * (wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS));
     Rj[t] = -(j1 + j2 + j3) * hh;
+  }
+}
+
+// hybrid.jl:136-146 at one point (compass names: E = i+1, N = j+1), per-term gg.
+__device__ __forceinline__ double hybrid_jac_point(double wE, double wW, double wN, double wS,
+                                                   double wNE, double wSW, double wNW,
+                                                   double wSE, double sE, double sW, double sN,
+                                                   double sS, double sNE, double sSW,
+                                                   double sNW, double sSE, double gg,
+                                                   double hh) {
+  const double j1 = gg * ((wE - wW) * (sN - sS) - (wN - wS) * (sE - sW));
+  const double j2 =
+      gg * (wE * (sNE - sSE) - wW * (sNW - sSW) - wN * (sNE - sNW) + wS * (sSE - sSW));
+  const double j3 =
+      gg * (wNE * (sN - sE) - wSW * (sW - sS) - wNW * (sN - sW) + wSE * (sE - sS));
+  return -(j1 + j2 + j3) * hh;
+}
+
+// The same as hybrid_jac_real_kernel in the shape of the vortex-merger row-group stage kernel
+// (vm_kernels.hip): a 256-thread workgroup owns 512 consecutive x of 2 consecutive rows, two
+// x per lane, the 4 rows it needs loaded at once (16 B per lane); workgroups in row-major
+// order, so the three streams advance through HBM sequentially.  x-neighbours by lane
+// shuffles, across wavefronts through LDS, the workgroup's two periodic halo columns by one
+// masked load.  nx a multiple of 512, ny even.
+__global__ __launch_bounds__(256) void hybrid_jac_tile_kernel(const double* __restrict__ Rw,
+                                                              const double* __restrict__ Rs,
+                                                              double* __restrict__ Rj, int nx,
+                                                              int ny, double inv_n, double gg,
+                                                              double hh) {
+  constexpr int G = 2, NR = G + 2, NW = 256 / kWave, TC = 512, XCDS = 8;
+  __shared__ double left[NW][2 * NR], right[NW][2 * NR];
+  const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+  const int strips = nx / TC;
+  // workgroup b runs on XCD b % 8; the row groups above and below share halo rows and should
+  // meet in one L2: automatic for 8 strips, else XCD (strip, band) walks a band of rows
+  int strip = blockIdx.x % strips, grp = blockIdx.x / strips;
+  if (strips < XCDS && XCDS % strips == 0) {
+    const int bands = XCDS / strips, ngrp = ny / G;
+    if (ngrp % bands == 0) {
+      const int xcd = blockIdx.x % XCDS, i = blockIdx.x / XCDS;
+      strip = xcd % strips;
+      grp = (xcd / strips) * (ngrp / bands) + i;
+    }
+  }
+  const int x0 = strip * TC, x = x0 + 2 * (int)threadIdx.x, y0 = grp * G;
+  auto row = [&](const double* a, int y) {
+    return a + (size_t)(y < 0 ? y + ny : (y >= ny ? y - ny : y)) * nx;
+  };
+  double2 wv[NR], sv[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    wv[j] = *reinterpret_cast<const double2*>(row(Rw, y0 - 1 + j) + x);
+    sv[j] = *reinterpret_cast<const double2*>(row(Rs, y0 - 1 + j) + x);
+  }
+  static_assert(4 * NR <= kWave, "halo fetch needs one lane per value");
+  double halo = 0.0;
+  const int side = threadIdx.x / (2 * NR), rem = threadIdx.x % (2 * NR);
+  if (threadIdx.x < 4 * NR) {
+    const int xh = side == 0 ? (x0 == 0 ? nx - 1 : x0 - 1) : (x0 + TC >= nx ? x0 + TC - nx : x0 + TC);
+    halo = row((rem & 1) ? Rs : Rw, y0 - 1 + rem / 2)[xh];
+  }
+  if ((lane == 0 && wave > 0) || (lane == kWave - 1 && wave < NW - 1)) {
+    double* e = lane == 0 ? right[wave - 1] : left[wave + 1];
+#pragma unroll
+    for (int j = 0; j < NR; ++j) {
+      e[2 * j] = lane == 0 ? wv[j].x : wv[j].y;
+      e[2 * j + 1] = lane == 0 ? sv[j].x : sv[j].y;
+    }
+  }
+  if (threadIdx.x < 4 * NR) (side == 0 ? left[0] : right[NW - 1])[rem] = halo;
+  __syncthreads();
+  Win ww[NR], sw[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    ww[j].l = __shfl_up(wv[j].y, 1, kWave);
+    ww[j].r = __shfl_down(wv[j].x, 1, kWave);
+    sw[j].l = __shfl_up(sv[j].y, 1, kWave);
+    sw[j].r = __shfl_down(sv[j].x, 1, kWave);
+    if (lane == 0) {
+      ww[j].l = left[wave][2 * j];
+      sw[j].l = left[wave][2 * j + 1];
+    }
+    if (lane == kWave - 1) {
+      ww[j].r = right[wave][2 * j];
+      sw[j].r = right[wave][2 * j + 1];
+    }
+    // w = real(ifft(.)): the transform's output times 1 / (nx ny)
+    ww[j] = Win{ww[j].l * inv_n, wv[j].x * inv_n, wv[j].y * inv_n, ww[j].r * inv_n};
+    sw[j] = Win{sw[j].l * inv_n, sv[j].x * inv_n, sv[j].y * inv_n, sw[j].r * inv_n};
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    const Win &wm = ww[j], &wc = ww[j + 1], &wp = ww[j + 2];
+    const Win &sm = sw[j], &sc = sw[j + 1], &sp = sw[j + 2];
+    double2 o;
+    o.x = hybrid_jac_point(wc.b, wc.l, wp.a, wm.a, wp.b, wm.l, wp.l, wm.b, sc.b, sc.l, sp.a,
+                           sm.a, sp.b, sm.l, sp.l, sm.b, gg, hh);
+    o.y = hybrid_jac_point(wc.r, wc.a, wp.b, wm.b, wp.r, wm.a, wp.a, wm.r, sc.r, sc.a, sp.b,
+                           sm.b, sp.r, sm.a, sp.a, sm.r, gg, hh);
+    *reinterpret_cast<double2*>(Rj + (size_t)(y0 + j) * nx + x) = o;
   }
 }
 
@@ -348,9 +449,10 @@ struct cfdj_spec {
       // column-pass scratch of both directions
       if (kind == CFDJ_SPEC_HYBRID) {
         launch_half_c2r2d(ha, kHalfHybrid, wf, X, R, stream);
-        hipLaunchKernelGGL(hybrid_jac_real_kernel, dim3(grid_for(n())), dim3(256), 0, stream, R,
-                           R + n(), Rj, nx, ny, 1.0 / ((double)nx * ny), 1.0 / (4.0 * dx * dy),
-                           1.0 / 3.0);
+        // half2d_supported: nx a multiple of 512, ny even
+        hipLaunchKernelGGL(hybrid_jac_tile_kernel, dim3((nx / 512) * (ny / 2)), dim3(256), 0,
+                           stream, R, R + n(), Rj, nx, ny, 1.0 / ((double)nx * ny),
+                           1.0 / (4.0 * dx * dy), 1.0 / 3.0);
       } else {
         launch_half_c2r2d(ha, kHalfPs23, wf, X, R, stream);
         hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
