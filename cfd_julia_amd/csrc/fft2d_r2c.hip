@@ -41,8 +41,11 @@ __device__ __forceinline__ double2 half_factor(double2 w, int arr, int m, int k,
   } else {
     const double kxm = a.kx[m], kyk = a.kx[k];
     const double k2 = kxm * kxm + kyk * kyk;
+    // x / k2 as x * (1 / k2), the reciprocal within an ulp (recip_nr): one rounding more than
+    // the reference's division, far inside the transforms' own round-off
+    const double ik2 = recip_nr(k2);
     if constexpr (MODE == kHalfHybrid) {  // hybrid.jl:103,115: w_f, w_f / k2
-      return arr == 0 ? w : make_double2(w.x / k2, w.y / k2);
+      return arr == 0 ? w : make_double2(w.x * ik2, w.y * ik2);
     } else {  // pseudospectral_23_rule.jl:109-133, arrays j1f..j4f
       // real(ifft(.)) keeps the Hermitian part of the filtered derivative spectrum
       // F g w_f, g = i kappa (/ k2): with w_f Hermitian that is i keff w_f (/ k2),
@@ -59,7 +62,7 @@ __device__ __forceinline__ double2 half_factor(double2 w, int arr, int m, int k,
       const double kap_m = fm ? (xder ? a.kx[mq] : a.kx[kq]) : 0.0;
       const double keff = 0.5 * (kap_p - kap_m);
       const double2 d = make_double2(keff * -w.y, keff * w.x);  // 1im * w_f * k
-      return (arr == 0 || arr == 2) ? make_double2(d.x / k2, d.y / k2) : d;
+      return (arr == 0 || arr == 2) ? make_double2(d.x * ik2, d.y * ik2) : d;
     }
   }
 }
@@ -147,58 +150,79 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
   }
 }
 
+#ifndef CFDJ_HALF_COLS_WAVES
+#define CFDJ_HALF_COLS_WAVES 4
+#endif
 template <int M, int MODE>
-__global__ __launch_bounds__(Plan<M>::T) void half_cols_kernel(const HalfSpecArgs a,
+__global__ __launch_bounds__(Plan<M>::T)
+    __attribute__((amdgpu_waves_per_eu(CFDJ_HALF_COLS_WAVES, CFDJ_HALF_COLS_WAVES))) void half_cols_kernel(const HalfSpecArgs a,
                                                              const double2* __restrict__ src,
-                                                             double2* __restrict__ dst, int nb) {
+                                                             double2* __restrict__ dst, int arr0,
+                                                             int nb) {
   using P = Plan<M>;
   static_assert(P::NSTAGES >= 2, "column length");
   constexpr int L = M / 2;
   __shared__ double lds[P::PAD];
   const int tid = threadIdx.x;
-  // the arrays of one column are neighbours in the launch order and on one XCD: the column
-  // is read from HBM once and from that L2 by the others
-  const int id = xcd_remap(blockIdx.x, gridDim.x);
-  const int m = __builtin_amdgcn_readfirstlane(id / nb), arr = __builtin_amdgcn_readfirstlane(id % nb);
-  double2* out = dst + (size_t)arr * L * M;
-  if constexpr (MODE == kHalfPs23) {
-    // columns the 2/3 rule zeroes on both sides (+m and -m): no transform
-    if (m > a.tx0) {
-      for (int k = tid; k < M; k += P::T) out[xidx<M>(m, k)] = make_double2(0.0, 0.0);
-      return;
+  // A workgroup forms `nb` arrays [arr0, arr0 + nb) of its column one after the other, the
+  // gridDim.x / L workgroups of a column are neighbours on one XCD.  With four arrays at
+  // 4096^2 one workgroup per column is fastest (186 against 203 us per launch: the column
+  // comes from HBM once and from L2 after that); with two arrays, or on smaller grids that
+  // need the workgroups to fill the chip, one workgroup per array.
+  const int id = xcd_remap(blockIdx.x, gridDim.x), per_col = gridDim.x / L;
+  const int m = __builtin_amdgcn_readfirstlane(id / per_col);
+  arr0 += __builtin_amdgcn_readfirstlane(id % per_col) * nb;
+#pragma unroll 1
+  for (int arr = arr0; arr < arr0 + nb; ++arr) {
+    double2* out = dst + (size_t)arr * L * M;
+    if constexpr (MODE == kHalfPs23) {
+      // columns the 2/3 rule zeroes on both sides (+m and -m): no transform
+      if (m > a.tx0) {
+        for (int k = tid; k < M; k += P::T) out[xidx<M>(m, k)] = make_double2(0.0, 0.0);
+        continue;
+      }
     }
+    // an opaque copy of the thread index per array: what depends only on it (twiddles,
+    // offsets) is formed again inside each pass instead of staying live across the loop
+    int t = tid;
+    asm volatile("" : "+v"(t));
+    if (m == 0) half_column<M, MODE, true>(lds, a, src, out, m, arr, t);
+    else half_column<M, MODE, false>(lds, a, src, out, m, arr, t);
   }
-  if (m == 0) {
-    half_column<M, MODE, true>(lds, a, src, out, m, arr, tid);
-    return;
-  }
-  half_column<M, MODE, false>(lds, a, src, out, m, arr, tid);
 }
 
 template <int M>
-void launch_half_cols(int mode, const HalfSpecArgs& a, const double2* src, double2* dst, int nb,
-                      hipStream_t st) {
-  const dim3 grid((unsigned)((M / 2) * nb)), block(Plan<M>::T);
+void launch_half_cols(int mode, const HalfSpecArgs& a, const double2* src, double2* dst, int arr0,
+                      int nb, hipStream_t st) {
+  const int per_wg = (M >= 4096 && nb > 2) ? nb : 1;  // arrays per workgroup
+  const dim3 grid((unsigned)((M / 2) * (nb / per_wg))), block(Plan<M>::T);
+  nb = per_wg;
   switch (mode) {
-    case 0: hipLaunchKernelGGL((half_cols_kernel<M, 0>), grid, block, 0, st, a, src, dst, nb); break;
+    case 0:
+      hipLaunchKernelGGL((half_cols_kernel<M, 0>), grid, block, 0, st, a, src, dst, arr0, nb);
+      break;
     case kHalfPlain:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPlain>), grid, block, 0, st, a, src, dst, nb);
+      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPlain>), grid, block, 0, st, a, src, dst, arr0,
+                         nb);
       break;
     case kHalfHybrid:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid>), grid, block, 0, st, a, src, dst, nb);
+      hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid>), grid, block, 0, st, a, src, dst,
+                         arr0, nb);
       break;
     default:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23>), grid, block, 0, st, a, src, dst, nb);
+      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23>), grid, block, 0, st, a, src, dst, arr0,
+                         nb);
       break;
   }
 }
 
-void half_cols(int mode, const HalfSpecArgs& a, const double2* src, double2* dst, int nb,
-               hipStream_t st) {
+// Arrays [arr0, arr0 + nb) of the mode.
+void half_cols(int mode, const HalfSpecArgs& a, const double2* src, double2* dst, int arr0,
+               int nb, hipStream_t st) {
   switch (a.n) {
-    case 1024: launch_half_cols<1024>(mode, a, src, dst, nb, st); break;
-    case 2048: launch_half_cols<2048>(mode, a, src, dst, nb, st); break;
-    default: launch_half_cols<4096>(mode, a, src, dst, nb, st); break;
+    case 1024: launch_half_cols<1024>(mode, a, src, dst, arr0, nb, st); break;
+    case 2048: launch_half_cols<2048>(mode, a, src, dst, arr0, nb, st); break;
+    default: launch_half_cols<4096>(mode, a, src, dst, arr0, nb, st); break;
   }
   CFDJ_HIP(hipGetLastError());
 }
@@ -233,7 +257,7 @@ void launch_half_r2c2d(const HalfSpecArgs& a, const double* r, double2* scratch,
                        hipStream_t st) {
   check(a);
   launch_fused_poisson_pass(0, row_args(a, r, nullptr, scratch), st);
-  half_cols(0, a, scratch, hs, 1, st);
+  half_cols(0, a, scratch, hs, 0, 1, st);
 }
 
 void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, double2* x, double* r,
@@ -242,8 +266,8 @@ void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, doubl
   if (mode != kHalfPlain && mode != kHalfHybrid && mode != kHalfPs23)
     throw Error{CFDJ_ERR_ARG, "half-spectrum transform: bad mode"};
   const int nb = arrays_of(mode);
-  half_cols(mode, a, hs, x, nb, st);
   const size_t half = (size_t)(a.n / 2) * a.n, full = (size_t)a.n * a.n;
+  half_cols(mode, a, hs, x, 0, nb, st);
   for (int b = 0; b < nb; ++b)
     launch_fused_poisson_pass(2, row_args(a, nullptr, r + b * full, x + b * half), st);
 }
