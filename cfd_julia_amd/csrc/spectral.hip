@@ -3,11 +3,20 @@
 //   22_NS2D_PseudoSpectral_23_Rule/pseudospectral_23_rule.jl (CFDJ_SPEC_PS23)
 //   21_NS2D_PseudoSpectral_32_Rule/pseudospectral_32_rule.jl (CFDJ_SPEC_PS32)
 //
-// All three advance the full complex vorticity spectrum w_f (nx x ny, column-major like
-// the reference's Array{ComplexF64}) with the same low-storage RK3 / Crank-Nicolson loop
-// (hybrid.jl:41-67) and differ in the Jacobian jf = fft(-J(w, psi)).  The reference never
-// assumes Hermitian symmetry (kx[1] = eps and its Nyquist derivatives are not odd), so the
-// transforms here are rocFFT complex-to-complex, with real(ifft(.)) taken as written.
+// All three advance the vorticity spectrum w_f with the same low-storage RK3 /
+// Crank-Nicolson loop (hybrid.jl:41-67) and differ in the Jacobian jf = fft(-J(w, psi)).
+//
+// The reference holds full complex nx x ny spectra and never assumes Hermitian symmetry (its
+// kx[1] = eps and its Nyquist derivatives are not odd, the 2/3 rule's zero band is not
+// symmetric) but takes real(ifft(.)) of everything, which keeps exactly the Hermitian part.
+// Three transform paths, the same results to FFT round-off:
+//   * square power-of-two grids of 1024..4096, hybrid and 2/3 rule: the state is the HALF
+//     spectrum (kx index 0..nx/2, ky contiguous) and the transforms are real (fft2d_r2c.hip;
+//     its column pass forms that Hermitian part from the half spectrum);
+//   * other power-of-two grids of 256..4096 (or CFDJ_SPEC_HALF=0): full spectra, the
+//     hand-written two-pass complex transform (fft2d_c2c.hip), real physical-space fields;
+//   * everything else (and the 3/2 rule's padded product grid): rocFFT complex-to-complex.
+// The C interface always speaks the reference's layout: complex nx x ny, kx contiguous.
 //
 // Per Jacobian evaluation (one RK3 substep):
 //   hybrid: [w_f, w_f / k2] -> batch-2 inverse c2c -> Arakawa stencil on the real parts
