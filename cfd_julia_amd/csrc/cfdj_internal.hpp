@@ -158,6 +158,7 @@ struct FusedPoissonArgs {
   bool neg;
   bool recip;           // see DivideParams::recip
   int ncu;              // compute units (persistent grid size)
+  int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
 };
 bool fused_poisson_supported(int nx, int ny, int rows);
 bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)

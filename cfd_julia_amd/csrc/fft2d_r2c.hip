@@ -176,9 +176,11 @@ __global__ __launch_bounds__(Plan<M>::T)
   for (int arr = arr0; arr < arr0 + nb; ++arr) {
     double2* out = dst + (size_t)arr * L * M;
     if constexpr (MODE == kHalfPs23) {
-      // columns the 2/3 rule zeroes on both sides (+m and -m): no transform
+      // columns the 2/3 rule zeroes on both sides (+m and -m): nothing to transform, and the
+      // row pass does not read them (band limit tx0)
       if (m > a.tx0) {
-        for (int k = tid; k < M; k += P::T) out[xidx<M>(m, k)] = make_double2(0.0, 0.0);
+        if constexpr (kTile8)
+          for (int k = tid; k < M; k += P::T) out[xidx<M>(m, k)] = make_double2(0.0, 0.0);
         continue;
       }
     }
@@ -268,8 +270,11 @@ void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, doubl
   const int nb = arrays_of(mode);
   const size_t half = (size_t)(a.n / 2) * a.n, full = (size_t)a.n * a.n;
   half_cols(mode, a, hs, x, 0, nb, st);
-  for (int b = 0; b < nb; ++b)
-    launch_fused_poisson_pass(2, row_args(a, nullptr, r + b * full, x + b * half), st);
+  for (int b = 0; b < nb; ++b) {
+    FusedPoissonArgs p = row_args(a, nullptr, r + b * full, x + b * half);
+    if (mode == kHalfPs23 && !kTile8) p.mmax = a.tx0;
+    launch_fused_poisson_pass(2, p, st);
+  }
 }
 
 }  // namespace cfdj

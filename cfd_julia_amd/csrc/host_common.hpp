@@ -287,6 +287,7 @@ struct Fused {
     a.neg = neg;
     a.recip = sym.kind == kSymbolDirichletExt;
     a.ncu = ncu;
+    a.mmax = 0;
     return a;
   }
   FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H,

@@ -523,10 +523,12 @@ constexpr int rows_np_xr() {
   return TILE ? (byT > 1 ? byT : 1) : (byT > CFDJ_ROWS_NP_XR_MIN ? byT : CFDJ_ROWS_NP_XR_MIN);
 }
 
-template <int L, int XR, bool TILE>
+// BAND: the spectrum is zero in the columns above `mmax` (the spectral solvers' 2/3 rule):
+// they are not read.
+template <int L, int XR, bool TILE, bool BAND = false>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
-    const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_, int mmax) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -549,8 +551,10 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     int qq, m;
     pair(i, qq, m);
     const bool z0 = i == 0 && m == 0;
-    const double2 Xm = base[(unsigned)sidx<TILE>(m, qq, M)];
-    const double2 Xq = base[(unsigned)sidx<TILE>(z0 ? L / 2 : L - m, qq, M)];
+    const int mq = z0 ? L / 2 : L - m;
+    double2 Xm = make_double2(0.0, 0.0), Xq = Xm;
+    if (!BAND || m <= mmax) Xm = base[(unsigned)sidx<TILE>(m, qq, M)];
+    if (!BAND || mq <= mmax) Xq = base[(unsigned)sidx<TILE>(mq, qq, M)];
     const double2 Xp = cconj(Xq);
     const double2 S = cadd(Xm, Xp);
     const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
@@ -693,14 +697,19 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
                              dim3(XR * Plan<L>::T), 0, st, a.f, a.H, a.rows, a.twL, a.twN);
         else
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN);
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0);
         return;
       }
     } else if (pass != 0 && L <= 2048) {
       constexpr int XR = rows_np_xr<L, false>();
       if (a.rows % XR == 0) {
-        hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false>), dim3(a.rows / XR),
-                           dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN);
+        if (a.mmax > 0)
+          hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false, true>), dim3(a.rows / XR),
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN,
+                             a.mmax);
+        else
+          hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false>), dim3(a.rows / XR),
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0);
         return;
       }
     }
@@ -766,6 +775,9 @@ void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t 
                                  (1 << a.rl_log2) <= a.ny
                            : fused_rows_supported(a.nx, a.rows);
   if (!ok) throw Error{CFDJ_ERR_ARG, "fused Poisson: unsupported size"};
+  // the band limit exists in the small-item inverse row kernel only
+  if (a.mmax > 0 && !(pass == 2 && !a.tile8 && a.nx <= 4096 && CFDJ_ROWS_INV_NP > 0))
+    throw Error{CFDJ_ERR_ARG, "fused Poisson: band limit unsupported here"};
   if (pass == 1) {
     switch (a.ny) {
       case 1024: launch_cols<1024>(a, st); break;

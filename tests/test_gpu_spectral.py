@@ -41,6 +41,36 @@ def test_gpu_spectral_jacobian_vs_oracle(spec, kind, n):
     assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
 
 
+@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+def test_gpu_spectral_jacobian_vs_oracle_4096(spec, kind):
+    """The benchmarked grid (4096^2, half-spectrum transforms) against the oracle's full
+    complex transforms, on a field with content in every mode up to the Nyquist row and
+    column: 1e-12 of max|jf| like the small grids."""
+    n = 4096
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    f = smooth_field(n, n, 6, n) + 0.01 * np.random.default_rng(n).standard_normal((n, n))
+    wf = so.to_spectral(f)
+    ref = so.JACOBIANS[KIND_ID[kind]](wf, so.wavespace(n, n, dx, dy), dx, dy)
+    with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+        got = h.jacobian(wf)
+    assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+def test_gpu_spectral_vm_steps_vs_oracle_1024(spec, kind):
+    """Vortex-merger steps on the half-spectrum path (n = 1024) against the oracle."""
+    n, steps, dt = 1024, 5, 1e-3
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    ref = so.numerical(w0, steps, dt, dx, dy, 1000.0, KIND_ID[kind])
+    with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+        h.upload_interior(w0)
+        h.step(dt, steps)
+        ut = h.download()
+    assert np.abs(ut[:n, :n] - ref).max() < 1e-10
+    assert np.array_equal(ut[n, :], ut[0, :]) and np.array_equal(ut[:, n], ut[:, 0])
+
+
 @pytest.mark.parametrize("kind", KINDS)
 @pytest.mark.parametrize("n,steps,dt", [(128, 20, 0.01), (256, 10, 0.005)])
 def test_gpu_spectral_vm_steps_vs_oracle(spec, kind, n, steps, dt):
