@@ -6,6 +6,7 @@ Tolerances: one Jacobian evaluation 1e-12 relative to max|jf| (FFT round-off: ro
 pocketfft); vorticity after K steps L-inf < 1e-10 (north-star bound, |w| ~ 1); the
 Taylor-Green known answer (zero Jacobian, exact scheme decay) to 1e-12.
 """
+import functools
 import math
 
 import numpy as np
@@ -32,8 +33,7 @@ def spec():
 @pytest.mark.parametrize("n", [64, 96, 256, 1024])
 def test_gpu_spectral_jacobian_vs_oracle(spec, kind, n):
     dx, dy, _, _ = vo.vm_grid(n, n)
-    f = smooth_field(n, n, 6, n) + 0.01 * np.random.default_rng(n).standard_normal((n, n))
-    wf = so.to_spectral(f)
+    wf = _noisy_spectrum(n)
     k2 = so.wavespace(n, n, dx, dy)
     ref = so.JACOBIANS[KIND_ID[kind]](wf, k2, dx, dy)
     with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
@@ -41,19 +41,42 @@ def test_gpu_spectral_jacobian_vs_oracle(spec, kind, n):
     assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
-def test_gpu_spectral_jacobian_vs_oracle_4096(spec, kind):
-    """The benchmarked grid (4096^2, half-spectrum transforms) against the oracle's full
-    complex transforms, on a field with content in every mode up to the Nyquist row and
-    column: 1e-12 of max|jf| like the small grids."""
-    n = 4096
-    dx, dy, _, _ = vo.vm_grid(n, n)
+@functools.lru_cache(maxsize=1)
+def _noisy_spectrum(n):
     f = smooth_field(n, n, 6, n) + 0.01 * np.random.default_rng(n).standard_normal((n, n))
-    wf = so.to_spectral(f)
+    return so.to_spectral(f)
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+def test_gpu_spectral_jacobian_vs_oracle_2048(spec, kind):
+    """The half-spectrum transforms (n = 2048) against the oracle's full complex ones, on a
+    field with content in every mode up to the Nyquist row and column: 1e-12 of max|jf| like
+    the small grids."""
+    n = 2048
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    wf = _noisy_spectrum(n)
     ref = so.JACOBIANS[KIND_ID[kind]](wf, so.wavespace(n, n, dx, dy), dx, dy)
     with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
         got = h.jacobian(wf)
     assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+def test_gpu_spectral_jacobian_4096_half_vs_full_spectrum(spec, monkeypatch, kind):
+    """The benchmarked grid: the half-spectrum path against the full-spectrum complex
+    transforms (CFDJ_SPEC_HALF=0, itself checked against the oracle on the smaller grids) on
+    the same noisy field, 1e-12 of max|jf|."""
+    n = 4096
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    wf = _noisy_spectrum(n)
+    out = {}
+    for name, env in (("half", None), ("full", "0")):
+        monkeypatch.delenv("CFDJ_SPEC_HALF", raising=False)
+        if env is not None:
+            monkeypatch.setenv("CFDJ_SPEC_HALF", env)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+            out[name] = h.jacobian(wf)
+    assert np.abs(out["half"] - out["full"]).max() <= 1e-12 * np.abs(out["full"]).max()
 
 
 @pytest.mark.parametrize("kind", ["hybrid", "2/3"])
