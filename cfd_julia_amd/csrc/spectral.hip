@@ -310,6 +310,72 @@ __global__ void ps_unpad_kernel(const double2* __restrict__ Jp, double2* __restr
   }
 }
 
+// The 3/2 rule on the half spectrum of its padded grid (library real transforms): element
+// (a, b), a <= px/2, of the four padded derivative spectra, as the Hermitian part
+// (P(a, b) + conj P(-a, -b)) / 2 that real(ifft(.)) keeps of the reference's padded array P
+// (pseudospectral_32_rule.jl:109-154: corner blocks of i k w_f (/ k2), times (nxe nye) /
+// (nx ny); the -nx/2 modes sit on the negative side only, kx[1] = eps is not odd -- P is not
+// Hermitian).  D: 4 arrays of (px/2 + 1) x py, x contiguous.
+__global__ void ps32_derivs_half_kernel(const double2* __restrict__ wf,
+                                        const double* __restrict__ kx, double2* __restrict__ D,
+                                        int nx, int ny, int px, int py, double sc, double sd) {
+  const int pxh = px / 2 + 1;
+  const size_t nh = (size_t)pxh * py;
+  const int hx = nx / 2, hy = ny / 2, qx = px - hx, qy = py - hy;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < nh;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int a0 = (int)(t % pxh), b0 = (int)(t / pxh);
+    double2 acc[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc[q] = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int a = side ? (a0 == 0 ? 0 : px - a0) : a0, b = side ? (b0 == 0 ? 0 : py - b0) : b0;
+      if (!((a < hx || a >= qx) && (b < hy || b >= qy))) continue;
+      const int i = a < hx ? a : a - qx + hx, j = b < hy ? b : b - qy + hy;
+      const double kxi = kx[i], kyj = kx[j];
+      const double k2 = kxi * kxi + kyj * kyj;
+      const double2 iw = times_i(wf[(size_t)j * nx + i]);
+      double2 d[4];
+      d[0] = cdiv_r(cmul_r(kxi, iw), k2);  // 1im * wf * kx / k2
+      d[1] = cmul_r(kyj, iw);              // 1im * wf * ky
+      d[2] = cdiv_r(cmul_r(kyj, iw), k2);  // 1im * wf * ky / k2
+      d[3] = cmul_r(kxi, iw);              // 1im * wf * kx
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double2 p = make_double2(d[q].x * sc / sd, d[q].y * sc / sd);
+        acc[q].x += 0.5 * p.x;
+        acc[q].y += side ? -0.5 * p.y : 0.5 * p.y;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) D[q * nh + t] = acc[q];
+  }
+}
+
+// pseudospectral_32_rule.jl:171-178 from the half spectrum Jh ((px/2 + 1) x py) of the real
+// product: jf(i, j) = fft(product)(a, b) * (nx ny) / (nxe nye), (a, b) the padded index of
+// mode (i, j); a > px/2 is the conjugate of (-a, -b).
+__global__ void ps32_unpad_half_kernel(const double2* __restrict__ Jh, double2* __restrict__ jf,
+                                       int nx, int ny, int px, int py, double sd, double sc) {
+  const size_t n = (size_t)nx * ny;
+  const int pxh = px / 2 + 1;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const int hx = nx / 2, hy = ny / 2;
+    const int a = i < hx ? i : i - hx + (px - hx), b = j < hy ? j : j - hy + (py - hy);
+    double2 v;
+    if (a < pxh) {
+      v = Jh[(size_t)b * pxh + a];
+    } else {
+      v = Jh[(size_t)(b == 0 ? 0 : py - b) * pxh + (px - a)];
+      v.y = -v.y;
+    }
+    jf[t] = make_double2(v.x * sd / sc, v.y * sd / sc);
+  }
+}
+
 // hybrid.jl:44-67, one RK3 / Crank-Nicolson substep.  z = .5dt k2 / re, d = alpha z;
 // out = ((1 - d)/(1 + d)) * w + (cA * jA + cB * jB) / (1 + d)   (stage 1: cB = 0, no jB);
 // out[1,1] = 0 after stages 1 and 2.
@@ -431,6 +497,10 @@ struct cfdj_spec {
   // 2/3 rule): every spectrum above holds the modes kx index 0..nx/2 only, ky contiguous;
   // the C interface converts (CFDJ_SPEC_HALF=0 keeps the full spectra)
   bool half = false;
+  // 3/2 rule: library REAL transforms on the padded grid (half the work of the complex
+  // ones; any even grid); CFDJ_SPEC_REAL=0 or CFDJ_SPEC_FFT=rocfft keep the complex plans
+  bool real32 = false;
+  rocfft_plan inv_r = nullptr, fwd_r = nullptr;  // Z2D batch 4, D2Z on px x py
   Fused fz;
   HalfSpecArgs ha{};
   size_t nh() const { return (size_t)(nx / 2 + 1) * ny; }
@@ -492,6 +562,22 @@ struct cfdj_spec {
       return;
     }
     const bool r32 = kind == CFDJ_SPEC_PS32;
+    if (real32) {
+      const double sc = (double)px * py, sd = (double)nx * ny;
+      const size_t nhp = (size_t)(px / 2 + 1) * py;
+      hipLaunchKernelGGL(ps32_derivs_half_kernel, dim3(grid_for(nhp)), dim3(256), 0, stream, wf,
+                         kx, X, nx, ny, px, py, sc, sd);
+      CFDJ_HIP(hipGetLastError());
+      plans.exec(inv_r, X, R);
+      hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
+                         1.0 / sc);
+      CFDJ_HIP(hipGetLastError());
+      plans.exec(fwd_r, Rj, J);
+      hipLaunchKernelGGL(ps32_unpad_half_kernel, dim3(grid_for(n())), dim3(256), 0, stream, J, jf,
+                         nx, ny, px, py, sd, sc);
+      CFDJ_HIP(hipGetLastError());
+      return;
+    }
     const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
     const int tx0 = nxe / 2, tx1 = nx - nxe / 2, ty0 = nye / 2, ty1 = ny - nye / 2;
     const double sc = (double)px * py, sd = (double)nx * ny;
@@ -638,12 +724,14 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
       h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,
                            ny - nye / 2};
     }
-    if (h->real_fields) {
-      h->R = dalloc<double>((size_t)nb * n);
-      h->Rj = dalloc<double>(n);
+    h->real32 = kind == CFDJ_SPEC_PS32 && want_hand && !(re_ && re_[0] == '0');
+    if (h->real_fields || h->real32) {
+      h->R = dalloc<double>((size_t)nb * np);
+      h->Rj = dalloc<double>(np);
     }
-    h->X = dalloc<double2>((size_t)nb * np);
-    if (kind == CFDJ_SPEC_PS32) h->J = dalloc<double2>(np);
+    const size_t nhp = (size_t)(h->px / 2 + 1) * h->py;  // half spectrum of the product grid
+    h->X = dalloc<double2>((size_t)nb * (h->real32 ? nhp : np));
+    if (kind == CFDJ_SPEC_PS32) h->J = dalloc<double2>(h->real32 ? nhp : np);
     h->field = dalloc<double>((size_t)(nx + 1) * (ny + 1));
     size_t lens[2] = {(size_t)nx, (size_t)ny};
     size_t lp[2] = {(size_t)h->px, (size_t)h->py};
@@ -651,11 +739,18 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
                           lens, 1, nullptr);
     h->inv = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
                           lens, 1, nullptr);
-    h->inv_b = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
-                            lp, nb, nullptr);
-    if (kind == CFDJ_SPEC_PS32)
+    if (!h->real32)
+      h->inv_b = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
+                              lp, nb, nullptr);
+    if (kind == CFDJ_SPEC_PS32 && !h->real32)
       h->fwd_p = h->plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace,
                               2, lp, 1, nullptr);
+    if (h->real32) {
+      h->inv_r = h->plans.add(rocfft_transform_type_real_inverse, rocfft_placement_notinplace,
+                              2, lp, nb, nullptr);
+      h->fwd_r = h->plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace,
+                              2, lp, 1, nullptr);
+    }
     h->plans.finalize(h->stream);
     *out = h.release();
   });
