@@ -15,7 +15,9 @@
 //     its column pass forms that Hermitian part from the half spectrum);
 //   * other power-of-two grids of 256..4096 (or CFDJ_SPEC_HALF=0): full spectra, the
 //     hand-written two-pass complex transform (fft2d_c2c.hip), real physical-space fields;
-//   * everything else (and the 3/2 rule's padded product grid): rocFFT complex-to-complex.
+//   * the 3/2 rule's padded product grid: rocFFT REAL transforms on the half spectrum of the
+//     padded grid (any even grid; CFDJ_SPEC_REAL=0: complex);
+//   * everything else: rocFFT complex-to-complex.
 // The C interface always speaks the reference's layout: complex nx x ny, kx contiguous.
 //
 // Per Jacobian evaluation (one RK3 substep):
