@@ -8,7 +8,7 @@
       RK3-CN step, MLUPS.
   Y   the multi-GPU y-slab code on one GPU (--virtual P): per-rank ms per step at the
       weak-scaling grids, i.e. the compute of one rank of an N-GPU run without the RCCL
-      latency (8192^2 / P = 2, 4; 16384^2 / P = 8).
+      latency (8192^2 / P = 2, 4, 8 -- P = 8 is BASELINE config 5; 16384^2 / P = 8).
 
   python tools/bench_secondary.py [--steps 20]
 """
@@ -108,7 +108,7 @@ def bench_slabs(steps=3):
     from cfd_julia_amd.common import vm_ic
 
     out = []
-    for n, P in ((8192, 2), (8192, 4), (16384, 8)):
+    for n, P in ((8192, 2), (8192, 4), (8192, 8), (16384, 8)):
         dx = 2 * math.pi / n
         dt = 5e-4 * 2.0 * 4096.0 ** 2 / (2 * n * n)
         with VortexMerger(n, n, dx, dx, 1000.0, kind="virtual", nranks=P) as h:
