@@ -43,16 +43,29 @@ def test_gpu_spectral_jacobian_vs_oracle(spec, kind, n):
 
 @functools.lru_cache(maxsize=1)
 def _noisy_spectrum(n):
-    f = smooth_field(n, n, 6, n) + 0.01 * np.random.default_rng(n).standard_normal((n, n))
-    return so.to_spectral(f)
+    """Spectrum of a smooth field plus white noise: content in every mode, Nyquist included.
+    From 2048 on the smooth part is set mode by mode in spectral space (smooth_field's 169
+    full-grid cos/sin passes take most of a minute at 4096^2)."""
+    rng = np.random.default_rng(n)
+    noise = 0.01 * rng.standard_normal((n, n))
+    if n < 2048:
+        return so.to_spectral(smooth_field(n, n, 6, n) + noise)
+    wf = np.fft.fft2(noise)
+    for kx in range(-6, 7):
+        for ky in range(-6, 7):
+            if (kx, ky) > (0, 0):  # one of each conjugate pair, its mirror set with it
+                c = complex(*rng.standard_normal(2)) * n * n / (1.0 + kx * kx + ky * ky)
+                wf[kx % n, ky % n] += c
+                wf[-kx % n, -ky % n] += np.conj(c)
+    return so.to_spectral(np.real(np.fft.ifft2(wf)))
 
 
 @pytest.mark.parametrize("kind", ["hybrid", "2/3"])
-def test_gpu_spectral_jacobian_vs_oracle_2048(spec, kind):
-    """The half-spectrum transforms (n = 2048) against the oracle's full complex ones, on a
-    field with content in every mode up to the Nyquist row and column: 1e-12 of max|jf| like
-    the small grids."""
-    n = 2048
+@pytest.mark.parametrize("n", [2048, 4096])
+def test_gpu_spectral_jacobian_vs_oracle_large(spec, kind, n):
+    """The half-spectrum transforms (n = 2048 and the benchmarked 4096) against the oracle's
+    full complex ones, on a field with content in every mode up to the Nyquist row and
+    column: 1e-12 of max|jf| like the small grids."""
     dx, dy, _, _ = vo.vm_grid(n, n)
     wf = _noisy_spectrum(n)
     ref = so.JACOBIANS[KIND_ID[kind]](wf, so.wavespace(n, n, dx, dy), dx, dy)
