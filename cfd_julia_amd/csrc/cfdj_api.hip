@@ -156,6 +156,12 @@ struct cfdj_vm {
   // ordered: the main stream waits for the omega halo before its first collective.
   hipStream_t side = nullptr;
   hipEvent_t ev_src = nullptr, ev_whalo = nullptr, ev_psi = nullptr, ev_shalo = nullptr;
+  // ... and the substructured solve's two all-gathers: the packed column's during the trace
+  // pass, the traces' during the packed column's own solve (gather_on_side, set by the
+  // overlapped stage); every RCCL operation of a step is then on the side stream, in program
+  // order, the same on every rank
+  hipEvent_t ev_g = nullptr, ev_g2 = nullptr, ev_t = nullptr, ev_t2 = nullptr;
+  bool gather_on_side = false;
   bool whalo_pending = false;
   double* gather = nullptr;                                      // Rccl download buffer
   // timing
@@ -432,7 +438,13 @@ struct cfdj_vm {
     for (auto& s : slabs)
       CFDJ_HIP(hipMemcpy2DAsync(G + s.row0, sizeof(double2), s.X, 8 * sizeof(double2),
                                 sizeof(double2), rows, hipMemcpyDeviceToDevice, stream));
-    if (mode == Mode::Rccl) {
+    const bool aside = gather_on_side && mode == Mode::Rccl;
+    if (aside) {
+      CFDJ_HIP(hipEventRecord(ev_g, stream));
+      CFDJ_HIP(hipStreamWaitEvent(side, ev_g, 0));
+      CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, side));
+      CFDJ_HIP(hipEventRecord(ev_g2, side));
+    } else if (mode == Mode::Rccl) {
       comm_order();
       CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, stream));
     }
@@ -445,10 +457,20 @@ struct cfdj_vm {
     if (mode == Mode::Rccl) {
       tbegin(CFDJ_K_COMM);
       const size_t cnt = (size_t)L * 4 * 2;  // doubles per rank
+      hipStream_t cs = stream;
+      if (aside) {
+        CFDJ_HIP(hipEventRecord(ev_t, stream));
+        CFDJ_HIP(hipStreamWaitEvent(side, ev_t, 0));
+        cs = side;
+      }
       CFDJ_NCCL(ncclAllGather(reinterpret_cast<double*>(T) + (size_t)rank * cnt, T, cnt,
-                              ncclDouble, comm, stream));
+                              ncclDouble, comm, cs));
+      if (aside) CFDJ_HIP(hipEventRecord(ev_t2, side));
       tend();
     }
+    // the packed column's solve needs the gathered column only; the interior solve the
+    // gathered traces only
+    if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_g2, 0));
     tbegin(CFDJ_K_DIVIDE);
     plans.exec(g_fwd, G, nullptr);
     PackedDivParams pd;
@@ -465,6 +487,7 @@ struct cfdj_vm {
     launch_packed_divide(pd, stream);
     plans.exec(g_inv, G, nullptr);
     tend();
+    if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_t2, 0));
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
       launch_schur_pass(1, schur_args(s), stream);
@@ -562,8 +585,15 @@ struct cfdj_vm {
     halo(false, {src}, side);
     CFDJ_HIP(hipEventRecord(ev_whalo, side));
     whalo_pending = true;
-    poisson({src}, true);
-    comm_order();  // paths without a collective before the psi halo
+    gather_on_side = use_schur;
+    try {
+      poisson({src}, true);
+    } catch (...) {
+      gather_on_side = false;
+      throw;
+    }
+    gather_on_side = false;
+    comm_order();  // paths without a collective on the main stream before the psi halo
     CFDJ_HIP(hipEventRecord(ev_psi, stream));
     CFDJ_HIP(hipStreamWaitEvent(side, ev_psi, 0));
     halo(true, {s.psi}, side);
@@ -773,7 +803,7 @@ struct cfdj_vm {
     dfree(d_flag);
     for (auto e : ev) (void)hipEventDestroy(e);
     if (side) (void)hipStreamSynchronize(side);
-    for (hipEvent_t e : {ev_src, ev_whalo, ev_psi, ev_shalo})
+    for (hipEvent_t e : {ev_src, ev_whalo, ev_psi, ev_shalo, ev_g, ev_g2, ev_t, ev_t2})
       if (e) (void)hipEventDestroy(e);
     if (side) (void)hipStreamDestroy(side);
     if (comm) ncclCommDestroy(comm);
@@ -1013,7 +1043,8 @@ int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double 
     const char* no_ov = std::getenv("CFDJ_NO_OVERLAP");
     if (!(no_ov && no_ov[0] == '1')) {
       CFDJ_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-      for (hipEvent_t* e : {&h->ev_src, &h->ev_whalo, &h->ev_psi, &h->ev_shalo})
+      for (hipEvent_t* e : {&h->ev_src, &h->ev_whalo, &h->ev_psi, &h->ev_shalo, &h->ev_g,
+                            &h->ev_g2, &h->ev_t, &h->ev_t2})
         CFDJ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
     }
     *out = h.release();
