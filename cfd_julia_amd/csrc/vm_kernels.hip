@@ -251,8 +251,18 @@ __global__ __launch_bounds__(256) void colsum_row_kernel(const double* __restric
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int x = blockIdx.x * 64 + lane;
   double s = 0.0;
-  if (x < nx)
-    for (int b = w; b < nb; b += 4) s += colpart[(size_t)b * nx + x];
+  if (x < nx) {
+    // eight loads in flight per lane, added in the order of the plain loop
+    int b = w;
+    for (; b + 28 < nb; b += 32) {
+      double v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = colpart[(size_t)(b + 4 * u) * nx + x];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; b < nb; b += 4) s += colpart[(size_t)b * nx + x];
+  }
   part[w][lane] = s;
   __syncthreads();
   if (x >= nx) return;
