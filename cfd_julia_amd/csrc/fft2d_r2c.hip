@@ -1,5 +1,5 @@
 // 2-D real <-> half-spectrum transforms of the spectral solvers (gfx950) for square
-// power-of-two grids of 1024..4096: 20_NS2D_Hybrid_Solver/hybrid.jl and
+// power-of-two grids of 1024..8192: 20_NS2D_Hybrid_Solver/hybrid.jl and
 // 22_NS2D_PseudoSpectral_23_Rule transform REAL fields (fft(complex(w, 0)), real(ifft(.))),
 // so the spectrum of every field they hold is Hermitian and half of it is enough: the modes
 // kx index m = 0..L (L = n/2), all ky.
@@ -73,6 +73,9 @@ __device__ __forceinline__ double2 half_factor(double2 w, int arr, int m, int k,
 #define CFDJ_HALF_TILE8 0
 #endif
 constexpr bool kTile8 = CFDJ_HALF_TILE8 != 0;
+// The inverse row pass skips the columns the 2/3 rule zeroes (its band limit) for rows of up
+// to 4096 reals in the column-major layout; elsewhere the column pass writes them as zeros.
+__host__ __device__ constexpr bool band_limited(int n) { return !kTile8 && n <= 4096; }
 template <int M>
 __device__ __forceinline__ size_t xidx(int m, int y) {
   if constexpr (kTile8) return ((((size_t)(m >> 3)) * M + y) << 3) + (m & 7);
@@ -179,7 +182,7 @@ __global__ __launch_bounds__(Plan<M>::T)
       // columns the 2/3 rule zeroes on both sides (+m and -m): nothing to transform, and the
       // row pass does not read them (band limit tx0)
       if (m > a.tx0) {
-        if constexpr (kTile8)
+        if constexpr (!band_limited(M))
           for (int k = tid; k < M; k += P::T) out[xidx<M>(m, k)] = make_double2(0.0, 0.0);
         continue;
       }
@@ -224,7 +227,8 @@ void half_cols(int mode, const HalfSpecArgs& a, const double2* src, double2* dst
   switch (a.n) {
     case 1024: launch_half_cols<1024>(mode, a, src, dst, arr0, nb, st); break;
     case 2048: launch_half_cols<2048>(mode, a, src, dst, arr0, nb, st); break;
-    default: launch_half_cols<4096>(mode, a, src, dst, arr0, nb, st); break;
+    case 4096: launch_half_cols<4096>(mode, a, src, dst, arr0, nb, st); break;
+    default: launch_half_cols<8192>(mode, a, src, dst, arr0, nb, st); break;
   }
   CFDJ_HIP(hipGetLastError());
 }
@@ -252,7 +256,8 @@ int arrays_of(int mode) { return mode == kHalfHybrid ? 2 : mode == kHalfPs23 ? 4
 }  // namespace
 
 bool half2d_supported(int nx, int ny) {
-  return nx == ny && (nx == 1024 || nx == 2048 || nx == 4096) && fused_rows_supported(nx, ny);
+  return nx == ny && (nx == 1024 || nx == 2048 || nx == 4096 || nx == 8192) &&
+         fused_rows_supported(nx, ny);
 }
 
 void launch_half_r2c2d(const HalfSpecArgs& a, const double* r, double2* scratch, double2* hs,
@@ -272,7 +277,7 @@ void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, doubl
   half_cols(mode, a, hs, x, 0, nb, st);
   for (int b = 0; b < nb; ++b) {
     FusedPoissonArgs p = row_args(a, nullptr, r + b * full, x + b * half);
-    if (mode == kHalfPs23 && !kTile8) p.mmax = a.tx0;
+    if (mode == kHalfPs23 && band_limited(a.n)) p.mmax = a.tx0;
     launch_fused_poisson_pass(2, p, st);
   }
 }

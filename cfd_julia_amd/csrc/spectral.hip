@@ -10,7 +10,7 @@
 // kx[1] = eps and its Nyquist derivatives are not odd, the 2/3 rule's zero band is not
 // symmetric) but takes real(ifft(.)) of everything, which keeps exactly the Hermitian part.
 // Three transform paths, the same results to FFT round-off:
-//   * square power-of-two grids of 1024..4096, hybrid and 2/3 rule: the state is the HALF
+//   * square power-of-two grids of 1024..8192, hybrid and 2/3 rule: the state is the HALF
 //     spectrum (kx index 0..nx/2, ky contiguous) and the transforms are real (fft2d_r2c.hip;
 //     its column pass forms that Hermitian part from the half spectrum);
 //   * other power-of-two grids of 256..4096 (or CFDJ_SPEC_HALF=0): full spectra, the
@@ -495,7 +495,7 @@ struct cfdj_spec {
   // real product (real_fields: CFDJ_SPEC_REAL=0 keeps them complex)
   double *R = nullptr, *Rj = nullptr;
   bool real_fields = false;
-  // half-spectrum state (fft2d_r2c.hip; square power-of-two grids of 1024..4096, hybrid and
+  // half-spectrum state (fft2d_r2c.hip; square power-of-two grids of 1024..8192, hybrid and
   // 2/3 rule): every spectrum above holds the modes kx index 0..nx/2 only, ky contiguous;
   // the C interface converts (CFDJ_SPEC_HALF=0 keeps the full spectra)
   bool half = false;
@@ -717,17 +717,19 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     if (h->hand_n) h->tw_n = twiddle_table(nx);
     if (h->hand_p) h->tw_p = (h->px == nx && h->tw_n) ? h->tw_n : twiddle_table(h->px);
     const char* re_ = std::getenv("CFDJ_SPEC_REAL");
-    h->real_fields = h->hand_n && h->px == nx && !(re_ && re_[0] == '0');
+    const bool want_real = !(re_ && re_[0] == '0');
+    h->real_fields = h->hand_n && h->px == nx && want_real;
     const char* he = std::getenv("CFDJ_SPEC_HALF");
-    h->half = h->real_fields && half2d_supported(nx, ny) && !(he && he[0] == '0');
+    h->half = want_hand && want_real && h->px == nx && half2d_supported(nx, ny) &&
+              !(he && he[0] == '0');
     if (h->half) {
       h->fz.init(nx, ny);
       const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
       h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,
                            ny - nye / 2};
     }
-    h->real32 = kind == CFDJ_SPEC_PS32 && want_hand && !(re_ && re_[0] == '0');
-    if (h->real_fields || h->real32) {
+    h->real32 = kind == CFDJ_SPEC_PS32 && want_hand && want_real;
+    if (h->real_fields || h->half || h->real32) {
       h->R = dalloc<double>((size_t)nb * np);
       h->Rj = dalloc<double>(np);
     }
@@ -737,11 +739,14 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     h->field = dalloc<double>((size_t)(nx + 1) * (ny + 1));
     size_t lens[2] = {(size_t)nx, (size_t)ny};
     size_t lp[2] = {(size_t)h->px, (size_t)h->py};
-    h->fwd = h->plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 2,
-                          lens, 1, nullptr);
-    h->inv = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
-                          lens, 1, nullptr);
-    if (!h->real32)
+    // library plans only where a path uses them (the half-spectrum path uses none)
+    if (!h->half) {
+      h->fwd = h->plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 2,
+                            lens, 1, nullptr);
+      h->inv = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
+                            lens, 1, nullptr);
+    }
+    if (!h->real32 && !h->half)
       h->inv_b = h->plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 2,
                               lp, nb, nullptr);
     if (kind == CFDJ_SPEC_PS32 && !h->real32)

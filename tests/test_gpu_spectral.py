@@ -93,6 +93,27 @@ def test_gpu_spectral_jacobian_4096_half_vs_full_spectrum(spec, monkeypatch, kin
 
 
 @pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+def test_gpu_spectral_8192_half_vs_library(spec, monkeypatch, kind):
+    """The largest grid of the half-spectrum path (8192^2: 4096-point half rows, 8192-point
+    columns, the inverse row pass without its band limit) against the library's complex
+    transforms: vortex-merger fields after 2 steps, 1e-12 of max|w|."""
+    n = 8192
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    out = {}
+    for name, env in (("half", None), ("rocfft", "rocfft")):
+        monkeypatch.delenv("CFDJ_SPEC_FFT", raising=False)
+        if env is not None:
+            monkeypatch.setenv("CFDJ_SPEC_FFT", env)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+            h.upload_interior(w0)
+            h.step(2.5e-4, 2)
+            out[name] = h.download()
+    assert np.isfinite(out["half"]).all()
+    assert np.abs(out["half"] - out["rocfft"]).max() <= 1e-12 * np.abs(out["rocfft"]).max()
+
+
+@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
 def test_gpu_spectral_vm_steps_vs_oracle_1024(spec, kind):
     """Vortex-merger steps on the half-spectrum path (n = 1024) against the oracle."""
     n, steps, dt = 1024, 5, 1e-3
