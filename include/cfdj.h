@@ -257,7 +257,7 @@ int cfdj_spec_step(cfdj_spec* h, double dt, int nsteps);
 int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu);
 /* w_f itself, complex nx x ny column-major as interleaved (re, im) doubles.  w_f is the
  * spectrum of a real field (the only kind the reference's loop produces): where the solver
- * keeps half of it (square power-of-two grids of 1024..4096, hybrid and 2/3 rule),
+ * keeps half of it (square power-of-two grids of 1024..8192, hybrid and 2/3 rule),
  * set_spectrum and jacobian read the modes kx index 0..nx/2 and take the others to be their
  * conjugate mirror, and get_spectrum returns exactly that mirror. */
 int cfdj_spec_get_spectrum(cfdj_spec* h, double* wf);
