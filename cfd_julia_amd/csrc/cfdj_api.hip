@@ -435,9 +435,7 @@ struct cfdj_vm {
     }
     // column m = 0 (packed DC / Nyquist) of the tiled spectrum: element j at 8 j
     tbegin(CFDJ_K_COMM);
-    for (auto& s : slabs)
-      CFDJ_HIP(hipMemcpy2DAsync(G + s.row0, sizeof(double2), s.X, 8 * sizeof(double2),
-                                sizeof(double2), rows, hipMemcpyDeviceToDevice, stream));
+    for (auto& s : slabs) launch_strided_copy(G + s.row0, 1, s.X, 8, rows, stream);
     const bool aside = gather_on_side && mode == Mode::Rccl;
     if (aside) {
       CFDJ_HIP(hipEventRecord(ev_g, stream));
@@ -494,9 +492,7 @@ struct cfdj_vm {
       tend();
     }
     tbegin(CFDJ_K_COMM);
-    for (auto& s : slabs)
-      CFDJ_HIP(hipMemcpy2DAsync(s.X, 8 * sizeof(double2), G + s.row0, sizeof(double2),
-                                sizeof(double2), rows, hipMemcpyDeviceToDevice, stream));
+    for (auto& s : slabs) launch_strided_copy(s.X, 8, G + s.row0, 1, rows, stream);
     tend();
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_INV);

@@ -103,6 +103,9 @@ void launch_colpart(const double* f, int nx, int rows, int rpw, double* colpart,
                     hipStream_t st);
 // out8[0][x] = sum over the nb blocks of colpart[b][x]; rows 1..7 of out8 zeroed.
 void launch_colsum_row(const double* colpart, int nb, int nx, double* out8, hipStream_t st);
+// dst[i ds] = src[i ss], i < n (complex elements).
+void launch_strided_copy(double2* dst, int ds, const double2* src, int ss, int n,
+                         hipStream_t st);
 
 // Spectral divide (Common.jl:118-121) on a (width x rows) block of the half spectrum
 // stored with row pitch `pitch` (complex elements); column i of the block is the

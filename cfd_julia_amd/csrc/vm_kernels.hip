@@ -390,6 +390,22 @@ void launch_colsum_row(const double* colpart, int nb, int nx, double* out8, hipS
   CFDJ_HIP(hipGetLastError());
 }
 
+// dst[i ds] = src[i ss], i < n (complex elements): column 0 of a tiled spectrum <-> a
+// contiguous column.
+__global__ __launch_bounds__(256) void strided_copy_kernel(double2* __restrict__ dst, int ds,
+                                                           const double2* __restrict__ src,
+                                                           int ss, int n) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[(size_t)i * ds] = src[(size_t)i * ss];
+}
+
+void launch_strided_copy(double2* dst, int ds, const double2* src, int ss, int n,
+                         hipStream_t st) {
+  hipLaunchKernelGGL(strided_copy_kernel, dim3((n + 255) / 256), dim3(256), 0, st, dst, ds, src,
+                     ss, n);
+  CFDJ_HIP(hipGetLastError());
+}
+
 void launch_divide(const DivideParams& p, hipStream_t st) {
   dim3 grid((p.width + 255) / 256, p.rows);
   hipLaunchKernelGGL(divide_kernel, grid, dim3(256), 0, st, p);
