@@ -13,7 +13,7 @@
 //          packed column's transform Z is split with its partner Z[-k] into the DC and the
 //          Nyquist column.
 // Inverse  (hs -> r): one column per workgroup and array: the column is read from hs,
-//          multiplied by the array's spectral factor (see HalfMode), inverse FFT along y,
+//          multiplied by the array's spectral factor (half_factor, modes kHalf*), inverse FFT along y,
 //          written to the scratch spectrum x; columns 0 and L are packed into column 0 as
 //          A + i B after projecting each onto its Hermitian part (A[k] + conj A[-k]) / 2 --
 //          what real(ifft(.)) keeps of them.  Then the Poisson solver's inverse row pass.
