@@ -90,14 +90,16 @@ def bench_spectral(steps=5):
         wn = np.zeros((n + 2, n + 2), order="F")
         vm_ic(n, n, x, x, wn)
         for kind in ("hybrid", "2/3", "3/2"):
+            k = steps if n > 1024 else 8 * steps
             with SpectralNS2D(n, n, dx, dx, 1000.0, kind) as h:
                 h.upload(wn)
-                h.step(1e-4, 1)
+                h.step(1e-4, 2)  # also captures the step's graph where it has one
                 t0 = time.perf_counter()
-                h.step(1e-4, steps)
+                h.step(1e-4, k)
                 t = time.perf_counter() - t0
-            out.append({"config": f"S {kind} {n}^2", "ms_per_step": round(t * 1e3 / steps, 3),
-                        "MLUPS": round(n * n * steps / t / 1e6, 1)})
+            out.append({"config": f"S {kind} {n}^2", "steps": k,
+                        "ms_per_step": round(t * 1e3 / k, 3),
+                        "MLUPS": round(n * n * k / t / 1e6, 1)})
     return out
 
 
