@@ -86,7 +86,7 @@ __device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __res
 #pragma unroll
   for (int b = 0; b < 16 / R0; ++b)
 #pragma unroll
-    for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[(unsigned)in_pos<L, 0>(tid, b, r)];
+    for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_stream(z + (unsigned)in_pos<L, 0>(tid, b, r));
 }
 
 // One work item (XR rows) of the forward row pass: stage 0 on the prefetched rows in `nxt`,
@@ -615,7 +615,8 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
 #pragma unroll
     for (int b = 0; b < 16 / R0; ++b)
 #pragma unroll
-      for (int r = 0; r < R0; ++r) v[b * R0 + r] = z[(unsigned)in_pos<L, 0>(tid, b, r)];
+      for (int r = 0; r < R0; ++r)
+        v[b * R0 + r] = load_stream(z + (unsigned)in_pos<L, 0>(tid, b, r));
   }
   stage_regs<L, 0, -1>(v, tid, twL);
   run_stages_half<L, 1, -1>(buf, v, tid, twL);

@@ -68,7 +68,8 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
     const Raw wr_n = fetch(row_ptr(p.w, p.w_lo, p.w_hi, yn, ny, nx), xs, xl, xr, is_l, is_r);
     const Raw sr_n = fetch(row_ptr(p.s, p.s_lo, p.s_hi, yn, ny, nx), xs, xl, xr, is_l, is_r);
     double2 wnv = make_double2(0.0, 0.0);
-    if constexpr (STAGE >= 2) wnv = *reinterpret_cast<const double2*>(p.wn + (size_t)y * nx + xs);
+    if constexpr (STAGE >= 2)
+      wnv = load_stream(reinterpret_cast<const double2*>(p.wn + (size_t)y * nx + xs));
 
     const Win wp = expand(wr_p, is_l, is_r);
     const Win sp = expand(sr_p, is_l, is_r);
@@ -166,7 +167,7 @@ __global__ __launch_bounds__(256) CFDJ_TILE_ATTR void vm_stage_tile_kernel(const
   for (int j = 0; j < G; ++j) {
     wnv[j] = make_double2(0.0, 0.0);
     if constexpr (STAGE >= 2)
-      wnv[j] = *reinterpret_cast<const double2*>(p.wn + (size_t)(y0 + j) * nx + x);
+      wnv[j] = load_stream(reinterpret_cast<const double2*>(p.wn + (size_t)(y0 + j) * nx + x));
   }
   // The two halo columns of the workgroup (periodic in x): one load in the first
   // wavefront, lane i < 4 NR fetching (side, row, field) = (i / 2NR, (i % 2NR) / 2, i % 2).
