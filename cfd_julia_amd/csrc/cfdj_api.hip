@@ -526,6 +526,7 @@ struct cfdj_vm {
     p.colpart = nullptr;
     p.rows_per_wave = rows_per_wave;
     p.march = stage_march;
+    p.stream = stream_loads_pay((size_t)nx * rows * sizeof(double));
     const double dx2 = dx * dx, dy2 = dy * dy;
     p.k.aa = 1.0 / (re * dx2);
     p.k.bb = 1.0 / (re * dy2);

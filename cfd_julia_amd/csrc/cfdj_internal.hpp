@@ -55,24 +55,39 @@ struct Error {
   } while (0)
 
 // ---- streaming loads ------------------------------------------------------------------
-// A 16-B load of data that is read once by one workgroup and not again soon (the forward row
-// pass's input, omega^n in the stage kernels): issued as a non-temporal load, so the line
-// does not displace what the next kernel re-reads (the half spectrum, psi) from the caches.
-// At 4096^2: step 0.776 -> 0.744 ms.  Not for lines several workgroups share (halo rows of
-// the stencil, the 32-B column pieces of the inverse row pass: 49 -> 84 us with it).
-// CFDJ_NT_LOADS=0 builds plain loads.
+// A load of data that is read once by one workgroup and not again soon (the forward row
+// pass's input, omega^n in the stage kernels, the spectral solvers' elementwise inputs):
+// with NT it is issued as a non-temporal load, so the line does not displace what the next
+// kernel re-reads (the half spectrum, psi) from the caches.  At 4096^2: step 0.776 -> 0.744
+// ms.  The host launches the NT instantiation of a kernel where the fields outgrow the 256 MB
+// last-level cache (stream_loads_pay); on grids that live in that cache the plain loads are
+// 3 % faster (and a run-time flag per load cost 1-2 % either way: a template flag).  Not
+// for lines several workgroups share (halo rows of the stencil, the 32-B column pieces of the
+// inverse row pass: 49 -> 84 us with it).  CFDJ_NT_LOADS=0 builds plain loads everywhere.
 #ifndef CFDJ_NT_LOADS
 #define CFDJ_NT_LOADS 1
 #endif
+template <bool NT>
 __device__ __forceinline__ double2 load_stream(const double2* p) {
 #if CFDJ_NT_LOADS
-  typedef double cfdj_d2v __attribute__((ext_vector_type(2)));
-  const cfdj_d2v t = __builtin_nontemporal_load(reinterpret_cast<const cfdj_d2v*>(p));
-  return make_double2(t.x, t.y);
-#else
-  return *p;
+  if constexpr (NT) {
+    typedef double cfdj_d2v __attribute__((ext_vector_type(2)));
+    const cfdj_d2v t = __builtin_nontemporal_load(reinterpret_cast<const cfdj_d2v*>(p));
+    return make_double2(t.x, t.y);
+  }
 #endif
+  return *p;
 }
+template <bool NT>
+__device__ __forceinline__ double load_stream(const double* p) {
+#if CFDJ_NT_LOADS
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+#endif
+  return *p;
+}
+// One field of `bytes` bytes among the half dozen a step cycles through: beyond 64 MB they do
+// not stay in the last-level cache from one kernel to the next anyway.
+inline bool stream_loads_pay(size_t bytes) { return bytes >= ((size_t)64 << 20); }
 
 // ---- XCD-aware block order ------------------------------------------------------------
 // Workgroups are dealt round-robin over the 8 XCDs (blocks b and b+8 share an XCD and its
@@ -100,6 +115,7 @@ struct StageCoef {
 // One slab of rows [0, ny) (local), pitch nx, x contiguous.  Row -1 / row ny are read
 // from the lo / hi ghost rows (on one GPU: the periodic wrap rows of the same array).
 struct StageParams {
+  bool stream = false;  // omega^n by streaming loads (load_stream)
   const double* w;     // stencil input omega_s
   const double* w_lo;
   const double* w_hi;
@@ -182,6 +198,7 @@ struct FusedPoissonArgs {
   bool recip;           // see DivideParams::recip
   int ncu;              // compute units (persistent grid size)
   int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
+  bool stream;          // pass 0: the input rows by streaming loads (load_stream)
 };
 bool fused_poisson_supported(int nx, int ny, int rows);
 bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)
@@ -238,6 +255,7 @@ struct HalfSpecArgs {
   int ncu;              // compute units (persistent row pass)
   const double* kx;     // wavenumbers (Common.jl:190-199), n entries; ky = kx
   int tx0, ty0, ty1;    // 2/3 rule: indices tx0 <= i < n - tx0, ty0 <= k < ty1 are zeroed
+  bool stream;          // once-read inputs by streaming loads (load_stream)
 };
 // Inverse modes: which arrays the column pass forms from the one spectrum w_f it reads.
 //   kHalfPlain  1 array : w_f

@@ -90,7 +90,7 @@ __device__ __forceinline__ double2 herm_part(double2 ck, double2 cq) {
 // One column (MODE 0: forward, H -> hs; else inverse, hs -> x).  EDGE = the packed column 0:
 // a separate instantiation of the whole body, so its extra loads do not set the register
 // count of the other L - 1 columns' code.
-template <int M, int MODE, bool EDGE>
+template <int M, int MODE, bool EDGE, bool NT>
 __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
                                             const double2* __restrict__ src,
                                             double2* __restrict__ dst, int m, int arr, int tid) {
@@ -107,7 +107,7 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
     for (int r = 0; r < R0; ++r) {
       const int k = in_pos<M, 0>(tid, b, r);
       if constexpr (MODE == 0) {
-        v[b * R0 + r] = src[xidx<M>(m, k)];
+        v[b * R0 + r] = load_stream<NT>(src + xidx<M>(m, k));  // scratch, dead after
       } else if constexpr (!EDGE) {
         v[b * R0 + r] = half_factor<MODE>(col[k], arr, m, k, a);
       } else {
@@ -156,7 +156,7 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
 #ifndef CFDJ_HALF_COLS_WAVES
 #define CFDJ_HALF_COLS_WAVES 4
 #endif
-template <int M, int MODE>
+template <int M, int MODE, bool NT>
 __global__ __launch_bounds__(Plan<M>::T)
     __attribute__((amdgpu_waves_per_eu(CFDJ_HALF_COLS_WAVES, CFDJ_HALF_COLS_WAVES))) void half_cols_kernel(const HalfSpecArgs a,
                                                              const double2* __restrict__ src,
@@ -191,8 +191,8 @@ __global__ __launch_bounds__(Plan<M>::T)
     // offsets) is formed again inside each pass instead of staying live across the loop
     int t = tid;
     asm volatile("" : "+v"(t));
-    if (m == 0) half_column<M, MODE, true>(lds, a, src, out, m, arr, t);
-    else half_column<M, MODE, false>(lds, a, src, out, m, arr, t);
+    if (m == 0) half_column<M, MODE, true, NT>(lds, a, src, out, m, arr, t);
+    else half_column<M, MODE, false, NT>(lds, a, src, out, m, arr, t);
   }
 }
 
@@ -203,20 +203,25 @@ void launch_half_cols(int mode, const HalfSpecArgs& a, const double2* src, doubl
   const dim3 grid((unsigned)((M / 2) * (nb / per_wg))), block(Plan<M>::T);
   nb = per_wg;
   switch (mode) {
-    case 0:
-      hipLaunchKernelGGL((half_cols_kernel<M, 0>), grid, block, 0, st, a, src, dst, arr0, nb);
+    case 0:  // the only mode with a streamed input (the scratch spectrum)
+      if (a.stream)
+        hipLaunchKernelGGL((half_cols_kernel<M, 0, true>), grid, block, 0, st, a, src, dst, arr0,
+                           nb);
+      else
+        hipLaunchKernelGGL((half_cols_kernel<M, 0, false>), grid, block, 0, st, a, src, dst, arr0,
+                           nb);
       break;
     case kHalfPlain:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPlain>), grid, block, 0, st, a, src, dst, arr0,
-                         nb);
+      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPlain, false>), grid, block, 0, st, a, src,
+                         dst, arr0, nb);
       break;
     case kHalfHybrid:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid>), grid, block, 0, st, a, src, dst,
-                         arr0, nb);
+      hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid, false>), grid, block, 0, st, a, src,
+                         dst, arr0, nb);
       break;
     default:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23>), grid, block, 0, st, a, src, dst, arr0,
-                         nb);
+      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23, false>), grid, block, 0, st, a, src, dst,
+                         arr0, nb);
       break;
   }
 }
@@ -241,6 +246,7 @@ FusedPoissonArgs row_args(const HalfSpecArgs& a, const double* f, double* s, dou
   p.s = s;
   p.H = p.C = H;
   p.tile8 = kTile8 ? 1 : 0;
+  p.stream = a.stream;
   p.twL = a.twL;
   p.twN = a.twN;
   p.ncu = a.ncu;

@@ -76,7 +76,7 @@ __device__ __forceinline__ size_t sidx(int m, int y, int M) {
 
 // Prefetch loads use a wave-uniform base pointer and unsigned 32-bit element offsets, so
 // each load needs one offset VGPR (global_load ... saddr) instead of a 64-bit address pair.
-template <int L>
+template <int L, bool NT>
 __device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __restrict__ f,
                                            int y, int tid) {
   // y is wave-uniform only when a row spans whole wavefronts (T >= 64)
@@ -86,7 +86,7 @@ __device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __res
 #pragma unroll
   for (int b = 0; b < 16 / R0; ++b)
 #pragma unroll
-    for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_stream(z + (unsigned)in_pos<L, 0>(tid, b, r));
+    for (int r = 0; r < R0; ++r) v[b * R0 + r] = load_stream<NT>(z + (unsigned)in_pos<L, 0>(tid, b, r));
 }
 
 // One work item (XR rows) of the forward row pass: stage 0 on the prefetched rows in `nxt`,
@@ -97,7 +97,7 @@ __device__ __forceinline__ void load_row_z(double2 (&v)[16], const double* __res
 // for the prefetched rows at the top of an item is then a counted `vmcnt` that leaves the
 // previous item's stores in flight -- their drain overlaps stage 0 instead of stalling it
 // (vmcnt completes in order; a conservative vmcnt(0) there cost a quarter of the pass).
-template <int L, bool TILE>
+template <int L, bool TILE, bool NT>
 __device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, double2* buf,
                                               const double* __restrict__ f,
                                               double2* __restrict__ H, int M, int y0,
@@ -107,7 +107,7 @@ __device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, 
   using C = RowCfg<L, true>;
   stage_regs<L, 0, -1>(nxt, tid, twL);
   lds_write<L, 0>(buf, nxt, tid);
-  if (next_y0 >= 0) load_row_z<L>(nxt, f, next_y0 + q, tid);
+  if (next_y0 >= 0) load_row_z<L, NT>(nxt, f, next_y0 + q, tid);
   __syncthreads();
   double2 v[16];
   run_stages<L, 1, -1, true>(buf, v, tid, twL);
@@ -146,7 +146,7 @@ __device__ __forceinline__ void rows_fwd_item(double2 (&nxt)[16], double2* lds, 
   __syncthreads();  // LDS is rewritten by the next item
 }
 
-template <int L, bool TILE>
+template <int L, bool TILE, bool NT>
 __global__ __launch_bounds__((RowCfg<L, true>::THREADS)) void rows_fwd_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
@@ -168,14 +168,14 @@ __global__ __launch_bounds__((RowCfg<L, true>::THREADS)) void rows_fwd_kernel(
   twN.fill(twN_);
   if (rg.count <= 0) return;
   double2 nxt[16];
-  load_row_z<L>(nxt, f, rg.first * C::XR + q, tid);
+  load_row_z<L, NT>(nxt, f, rg.first * C::XR + q, tid);
   __syncthreads();
   auto item_y0 = [&](int it) { return (rg.first + it * rg.stride) * C::XR; };
-  rows_fwd_item<L, TILE>(nxt, lds, buf, f, H, M, item_y0(0), rg.count > 1 ? item_y0(1) : -1, q,
-                         tid, twL, twN);
+  rows_fwd_item<L, TILE, NT>(nxt, lds, buf, f, H, M, item_y0(0),
+                             rg.count > 1 ? item_y0(1) : -1, q, tid, twL, twN);
   for (int it = 1; it < rg.count; ++it)
-    rows_fwd_item<L, TILE>(nxt, lds, buf, f, H, M, item_y0(it),
-                           it + 1 < rg.count ? item_y0(it + 1) : -1, q, tid, twL, twN);
+    rows_fwd_item<L, TILE, NT>(nxt, lds, buf, f, H, M, item_y0(it),
+                               it + 1 < rg.count ? item_y0(it + 1) : -1, q, tid, twL, twN);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -596,7 +596,7 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
 // four workgroups per CU), used with the 8-mode-tile layout of the y-slab path, where one
 // row's modes are whole 128-B lines; in the column-major layout a small item's column
 // segments are too short to write (see above) and the persistent kernel stays.
-template <int L, int XR, bool TILE>
+template <int L, int XR, bool TILE, bool NT>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
@@ -616,7 +616,7 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     for (int b = 0; b < 16 / R0; ++b)
 #pragma unroll
       for (int r = 0; r < R0; ++r)
-        v[b * R0 + r] = load_stream(z + (unsigned)in_pos<L, 0>(tid, b, r));
+        v[b * R0 + r] = load_stream<NT>(z + (unsigned)in_pos<L, 0>(tid, b, r));
   }
   stage_regs<L, 0, -1>(v, tid, twL);
   run_stages_half<L, 1, -1>(buf, v, tid, twL);
@@ -693,8 +693,11 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
     if (a.tile8) {
       constexpr int XR = rows_np_xr<L, true>();
       if (a.rows % XR == 0) {
-        if (pass == 0)
-          hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true>), dim3(a.rows / XR),
+        if (pass == 0 && a.stream)
+          hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, true>), dim3(a.rows / XR),
+                             dim3(XR * Plan<L>::T), 0, st, a.f, a.H, a.rows, a.twL, a.twN);
+        else if (pass == 0)
+          hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, false>), dim3(a.rows / XR),
                              dim3(XR * Plan<L>::T), 0, st, a.f, a.H, a.rows, a.twL, a.twN);
         else
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true>), dim3(a.rows / XR),
@@ -728,12 +731,18 @@ void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st) {
   const int per_cu = (160 * 1024) / row_lds;
   const dim3 grid(persistent_grid(a.ncu, per_cu, a.rows / C::XR));
   if constexpr (FWD) {
-    if (a.tile8)
-      hipLaunchKernelGGL((rows_fwd_kernel<L, true>), grid, dim3(C::THREADS), 0, st, a.f, a.H,
-                         a.rows, a.twL, a.twN);
+    if (a.tile8 && a.stream)
+      hipLaunchKernelGGL((rows_fwd_kernel<L, true, true>), grid, dim3(C::THREADS), 0, st, a.f,
+                         a.H, a.rows, a.twL, a.twN);
+    else if (a.tile8)
+      hipLaunchKernelGGL((rows_fwd_kernel<L, true, false>), grid, dim3(C::THREADS), 0, st, a.f,
+                         a.H, a.rows, a.twL, a.twN);
+    else if (a.stream)
+      hipLaunchKernelGGL((rows_fwd_kernel<L, false, true>), grid, dim3(C::THREADS), 0, st, a.f,
+                         a.H, a.rows, a.twL, a.twN);
     else
-      hipLaunchKernelGGL((rows_fwd_kernel<L, false>), grid, dim3(C::THREADS), 0, st, a.f, a.H,
-                         a.rows, a.twL, a.twN);
+      hipLaunchKernelGGL((rows_fwd_kernel<L, false, false>), grid, dim3(C::THREADS), 0, st, a.f,
+                         a.H, a.rows, a.twL, a.twN);
   } else {
     if (a.tile8)
       hipLaunchKernelGGL((rows_inv_kernel<L, true>), grid, dim3(C::THREADS), 0, st, a.H, a.s,

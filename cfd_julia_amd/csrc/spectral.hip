@@ -287,12 +287,16 @@ __global__ void ps_product_kernel(const double2* __restrict__ D, double2* __rest
 }
 
 // ... on real fields (the four real(ifft(.)) as real arrays), real product.
+template <bool NT>
 __global__ void ps_product_real_kernel(const double* __restrict__ D, double* __restrict__ Rj,
                                        size_t np, double inv_np) {
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < np;
        t += (size_t)gridDim.x * blockDim.x) {
-    const double j1 = D[t] * inv_np, j2 = D[np + t] * inv_np;
-    const double j3 = D[2 * np + t] * inv_np, j4 = D[3 * np + t] * inv_np;
+    // the four fields are read once: streaming loads (the product stays cached for the
+    // forward transform)
+    const double j1 = load_stream<NT>(D + t) * inv_np, j2 = load_stream<NT>(D + np + t) * inv_np;
+    const double j3 = load_stream<NT>(D + 2 * np + t) * inv_np;
+    const double j4 = load_stream<NT>(D + 3 * np + t) * inv_np;
     Rj[t] = j1 * j2 - j3 * j4;
   }
 }
@@ -382,7 +386,7 @@ __global__ void ps32_unpad_half_kernel(const double2* __restrict__ Jh, double2* 
 // out = ((1 - d)/(1 + d)) * w + (cA * jA + cB * jB) / (1 + d)   (stage 1: cB = 0, no jB);
 // out[1,1] = 0 after stages 1 and 2.
 // HALF: the arrays are half spectra ((nx/2 + 1) columns of ny, ky contiguous).
-template <int STAGE, bool HALF>
+template <int STAGE, bool HALF, bool NT>
 __global__ void cn_update_kernel(const double2* __restrict__ w, const double2* __restrict__ jA,
                                  const double2* __restrict__ jB, double2* __restrict__ out,
                                  const double* __restrict__ kx, int nx, int ny, double hdt,
@@ -396,10 +400,11 @@ __global__ void cn_update_kernel(const double2* __restrict__ w, const double2* _
     const double d = alpha * z;
     const double g = (1.0 - d) / (1.0 + d);
     const double e = 1.0 + d;
-    const double2 wv = w[t];
-    double2 f = cmul_r(cA, jA[t]);
+    // each read once and not again before the next transforms: streaming loads
+    const double2 wv = load_stream<NT>(w + t);
+    double2 f = cmul_r(cA, load_stream<NT>(jA + t));
     if constexpr (STAGE >= 2) {
-      const double2 fb = cmul_r(cB, jB[t]);
+      const double2 fb = cmul_r(cB, load_stream<NT>(jB + t));
       f = make_double2(f.x + fb.x, f.y + fb.y);
     }
     double2 o = make_double2(g * wv.x + f.x / e, g * wv.y + f.y / e);
@@ -499,6 +504,7 @@ struct cfdj_spec {
   // 2/3 rule): every spectrum above holds the modes kx index 0..nx/2 only, ky contiguous;
   // the C interface converts (CFDJ_SPEC_HALF=0 keeps the full spectra)
   bool half = false;
+  bool stream_loads = false;  // fields beyond the last-level cache: load_stream
   // 3/2 rule: library REAL transforms on the padded grid (half the work of the complex
   // ones; any even grid); CFDJ_SPEC_REAL=0 or CFDJ_SPEC_FFT=rocfft keep the complex plans
   bool real32 = false;
@@ -522,6 +528,16 @@ struct cfdj_spec {
   size_t n() const { return (size_t)nx * ny; }
   size_t np() const { return (size_t)px * py; }
 
+  // Rj = j1 j2 - j3 j4 of the four real fields in R.
+  void product_real(unsigned gb, double inv_np) {
+    if (stream_loads)
+      hipLaunchKernelGGL(ps_product_real_kernel<true>, dim3(gb), dim3(256), 0, stream, R, Rj,
+                         np(), inv_np);
+    else
+      hipLaunchKernelGGL(ps_product_real_kernel<false>, dim3(gb), dim3(256), 0, stream, R, Rj,
+                         np(), inv_np);
+  }
+
   // jf = fft(-J(w, psi)) of the spectrum wf (hybrid.jl:92-152 / pseudospectral_*.jl).
   void jacobian(const double2* wf, double2* jf) {
     const unsigned gb = grid_for(np());
@@ -536,8 +552,7 @@ struct cfdj_spec {
                            1.0 / (4.0 * dx * dy), 1.0 / 3.0);
       } else {
         launch_half_c2r2d(ha, kHalfPs23, wf, X, R, stream);
-        hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
-                           1.0 / ((double)px * py));
+        product_real(gb, 1.0 / ((double)px * py));
       }
       CFDJ_HIP(hipGetLastError());
       launch_half_r2c2d(ha, Rj, X, jf, stream);
@@ -571,8 +586,7 @@ struct cfdj_spec {
                          kx, X, nx, ny, px, py, sc, sd);
       CFDJ_HIP(hipGetLastError());
       plans.exec(inv_r, X, R);
-      hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
-                         1.0 / sc);
+      product_real(gb, 1.0 / sc);
       CFDJ_HIP(hipGetLastError());
       plans.exec(fwd_r, Rj, J);
       hipLaunchKernelGGL(ps32_unpad_half_kernel, dim3(grid_for(n())), dim3(256), 0, stream, J, jf,
@@ -588,8 +602,7 @@ struct cfdj_spec {
     CFDJ_HIP(hipGetLastError());
     if (real_fields && !r32) {  // 2/3 rule on a power-of-two grid: product grid = grid
       launch_c2r2d(X, R, nx, ny, nb, tw_n, tw_n, stream);
-      hipLaunchKernelGGL(ps_product_real_kernel, dim3(gb), dim3(256), 0, stream, R, Rj, np(),
-                         1.0 / sc);
+      product_real(gb, 1.0 / sc);
       CFDJ_HIP(hipGetLastError());
       launch_r2c2d(Rj, jf, nx, ny, 1, tw_n, tw_n, stream);
       return;
@@ -610,12 +623,16 @@ struct cfdj_spec {
   template <int STAGE>
   void update(const double2* w, const double2* jA, const double2* jB, double2* out, double dt,
               double alpha, double cA, double cB) {
-    if (half)
-      hipLaunchKernelGGL((cn_update_kernel<STAGE, true>), dim3(grid_for(nh())), dim3(256), 0,
-                         stream, w, jA, jB, out, kx, nx, ny, 0.5 * dt, re, alpha, cA, cB);
-    else
-      hipLaunchKernelGGL((cn_update_kernel<STAGE, false>), dim3(grid_for(n())), dim3(256), 0,
-                         stream, w, jA, jB, out, kx, nx, ny, 0.5 * dt, re, alpha, cA, cB);
+    const dim3 g(grid_for(half ? nh() : n())), b(256);
+    const double hdt = 0.5 * dt;
+#define CFDJ_CN(H, N)                                                                       \
+  hipLaunchKernelGGL((cn_update_kernel<STAGE, H, N>), g, b, 0, stream, w, jA, jB, out, kx, nx, \
+                     ny, hdt, re, alpha, cA, cB)
+    if (half && stream_loads) CFDJ_CN(true, true);
+    else if (half) CFDJ_CN(true, false);
+    else if (stream_loads) CFDJ_CN(false, true);
+    else CFDJ_CN(false, false);
+#undef CFDJ_CN
     CFDJ_HIP(hipGetLastError());
   }
 
@@ -716,6 +733,7 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     h->hand_p = want_hand && c2c2d_supported(h->px, h->py);
     if (h->hand_n) h->tw_n = twiddle_table(nx);
     if (h->hand_p) h->tw_p = (h->px == nx && h->tw_n) ? h->tw_n : twiddle_table(h->px);
+    h->stream_loads = stream_loads_pay(np * sizeof(double));
     const char* re_ = std::getenv("CFDJ_SPEC_REAL");
     const bool want_real = !(re_ && re_[0] == '0');
     h->real_fields = h->hand_n && h->px == nx && want_real;
@@ -726,7 +744,7 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
       h->fz.init(nx, ny);
       const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
       h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,
-                           ny - nye / 2};
+                           ny - nye / 2, h->stream_loads};
     }
     h->real32 = kind == CFDJ_SPEC_PS32 && want_hand && want_real;
     if (h->real_fields || h->half || h->real32) {

@@ -30,7 +30,7 @@ __device__ __forceinline__ const double* row_ptr(const double* a, const double* 
 // `rows_per_wave` rows in y with a 3-row register window of omega and psi; x-neighbours
 // come from lane shuffles, the two wave-edge values from one masked load each.  Four
 // independent wavefronts per 256-thread workgroup take four consecutive row chunks.
-template <int STAGE>
+template <int STAGE, bool NT>
 __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const StageParams p) {
   const int lane = threadIdx.x & (kWave - 1);
   const int wave = threadIdx.x / kWave;
@@ -69,7 +69,7 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
     const Raw sr_n = fetch(row_ptr(p.s, p.s_lo, p.s_hi, yn, ny, nx), xs, xl, xr, is_l, is_r);
     double2 wnv = make_double2(0.0, 0.0);
     if constexpr (STAGE >= 2)
-      wnv = load_stream(reinterpret_cast<const double2*>(p.wn + (size_t)y * nx + xs));
+      wnv = load_stream<NT>(reinterpret_cast<const double2*>(p.wn + (size_t)y * nx + xs));
 
     const Win wp = expand(wr_p, is_l, is_r);
     const Win sp = expand(sr_p, is_l, is_r);
@@ -128,7 +128,7 @@ constexpr int kTileRows = CFDJ_TILE_ROWS;
 constexpr int kTileCols = 512;
 constexpr int kXcds = 8;  // MI355X: workgroup b is dispatched to XCD b % 8
 
-template <int STAGE>
+template <int STAGE, bool NT>
 __global__ __launch_bounds__(256) CFDJ_TILE_ATTR void vm_stage_tile_kernel(const StageParams p) {
   constexpr int G = kTileRows, NR = G + 2, NW = 256 / kWave;
   // left[w]: the value left of wavefront w's first x (w = 0: the workgroup's halo column);
@@ -167,7 +167,7 @@ __global__ __launch_bounds__(256) CFDJ_TILE_ATTR void vm_stage_tile_kernel(const
   for (int j = 0; j < G; ++j) {
     wnv[j] = make_double2(0.0, 0.0);
     if constexpr (STAGE >= 2)
-      wnv[j] = load_stream(reinterpret_cast<const double2*>(p.wn + (size_t)(y0 + j) * nx + x));
+      wnv[j] = load_stream<NT>(reinterpret_cast<const double2*>(p.wn + (size_t)(y0 + j) * nx + x));
   }
   // The two halo columns of the workgroup (periodic in x): one load in the first
   // wavefront, lane i < 4 NR fetching (side, row, field) = (i / 2NR, (i % 2NR) / 2, i % 2).
@@ -353,10 +353,17 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
     if (blocks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
     const dim3 grid((unsigned)blocks), block(256);
     switch (stage) {
-      case 0: hipLaunchKernelGGL(vm_stage_tile_kernel<0>, grid, block, 0, st, p); break;
-      case 1: hipLaunchKernelGGL(vm_stage_tile_kernel<1>, grid, block, 0, st, p); break;
-      case 2: hipLaunchKernelGGL(vm_stage_tile_kernel<2>, grid, block, 0, st, p); break;
-      default: hipLaunchKernelGGL(vm_stage_tile_kernel<3>, grid, block, 0, st, p); break;
+      // stages 0 and 1 read no omega^n: one instantiation
+      case 0: hipLaunchKernelGGL((vm_stage_tile_kernel<0, false>), grid, block, 0, st, p); break;
+      case 1: hipLaunchKernelGGL((vm_stage_tile_kernel<1, false>), grid, block, 0, st, p); break;
+      case 2:
+        if (p.stream) hipLaunchKernelGGL((vm_stage_tile_kernel<2, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((vm_stage_tile_kernel<2, false>), grid, block, 0, st, p);
+        break;
+      default:
+        if (p.stream) hipLaunchKernelGGL((vm_stage_tile_kernel<3, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((vm_stage_tile_kernel<3, false>), grid, block, 0, st, p);
+        break;
     }
     CFDJ_HIP(hipGetLastError());
     return;
@@ -370,10 +377,16 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   dim3 grid((unsigned)(strips * chunks));
   dim3 block(kWave * kWavesPerBlock);
   switch (stage) {
-    case 0: hipLaunchKernelGGL(vm_stage_kernel<0>, grid, block, 0, st, p); break;
-    case 1: hipLaunchKernelGGL(vm_stage_kernel<1>, grid, block, 0, st, p); break;
-    case 2: hipLaunchKernelGGL(vm_stage_kernel<2>, grid, block, 0, st, p); break;
-    default: hipLaunchKernelGGL(vm_stage_kernel<3>, grid, block, 0, st, p); break;
+    case 0: hipLaunchKernelGGL((vm_stage_kernel<0, false>), grid, block, 0, st, p); break;
+    case 1: hipLaunchKernelGGL((vm_stage_kernel<1, false>), grid, block, 0, st, p); break;
+    case 2:
+      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<2, true>), grid, block, 0, st, p);
+      else hipLaunchKernelGGL((vm_stage_kernel<2, false>), grid, block, 0, st, p);
+      break;
+    default:
+      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<3, true>), grid, block, 0, st, p);
+      else hipLaunchKernelGGL((vm_stage_kernel<3, false>), grid, block, 0, st, p);
+      break;
   }
   CFDJ_HIP(hipGetLastError());
 }

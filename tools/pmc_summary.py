@@ -20,7 +20,8 @@ def per_kernel(path, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"]
+        # template flags after the first argument (", true") are not part of the key
+        name = re.sub(r"(<\d+)(?:, (?:true|false|\d+))+>", r"\1>", r["Kernel_Name"])
         m = re.search(r"(vm_stage_tile_kernel<\d>|vm_stage_kernel<\d>|rows_fwd_kernel<\d+>|cols_kernel<\d+>|"
                       r"rows_inv_kernel<\d+>|divide_kernel|\w+kernel\w*)", name)
         vals[m.group(1) if m else name[:60]].append(float(r["Counter_Value"]) * 1024.0)
