@@ -130,7 +130,7 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
 #pragma unroll
     for (int r = 0; r < RL; ++r) {
       if constexpr (MODE == 0) ocol[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
-      else dst[xidx<M>(m, out_pos<M, SL>(tid, b, r))] = v[b * RL + r];
+      else store_stream<NT>(dst + xidx<M>(m, out_pos<M, SL>(tid, b, r)), v[b * RL + r]);
     }
   if constexpr (MODE == 0 && EDGE) {
     // Z = FFT_y(X0 + i XL), X0 and XL real: F0[k] = (Z[k] + conj Z[-k]) / 2,
@@ -203,7 +203,7 @@ void launch_half_cols(int mode, const HalfSpecArgs& a, const double2* src, doubl
   const dim3 grid((unsigned)((M / 2) * (nb / per_wg))), block(Plan<M>::T);
   nb = per_wg;
   switch (mode) {
-    case 0:  // the only mode with a streamed input (the scratch spectrum)
+    case 0:  // NT = the input (the scratch spectrum, dead after this read) by streaming loads
       if (a.stream)
         hipLaunchKernelGGL((half_cols_kernel<M, 0, true>), grid, block, 0, st, a, src, dst, arr0,
                            nb);
@@ -211,17 +211,27 @@ void launch_half_cols(int mode, const HalfSpecArgs& a, const double2* src, doubl
         hipLaunchKernelGGL((half_cols_kernel<M, 0, false>), grid, block, 0, st, a, src, dst, arr0,
                            nb);
       break;
+    // inverse modes: NT = the scratch spectrum (134 MB per array at 4096^2, read back only
+    // after the whole pass) by streaming stores
     case kHalfPlain:
       hipLaunchKernelGGL((half_cols_kernel<M, kHalfPlain, false>), grid, block, 0, st, a, src,
                          dst, arr0, nb);
       break;
     case kHalfHybrid:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid, false>), grid, block, 0, st, a, src,
-                         dst, arr0, nb);
+      if (a.stream)
+        hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid, true>), grid, block, 0, st, a, src,
+                           dst, arr0, nb);
+      else
+        hipLaunchKernelGGL((half_cols_kernel<M, kHalfHybrid, false>), grid, block, 0, st, a, src,
+                           dst, arr0, nb);
       break;
     default:
-      hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23, false>), grid, block, 0, st, a, src, dst,
-                         arr0, nb);
+      if (a.stream)
+        hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23, true>), grid, block, 0, st, a, src,
+                           dst, arr0, nb);
+      else
+        hipLaunchKernelGGL((half_cols_kernel<M, kHalfPs23, false>), grid, block, 0, st, a, src,
+                           dst, arr0, nb);
       break;
   }
 }

@@ -322,6 +322,7 @@ __global__ void ps_unpad_kernel(const double2* __restrict__ Jp, double2* __restr
 // (pseudospectral_32_rule.jl:109-154: corner blocks of i k w_f (/ k2), times (nxe nye) /
 // (nx ny); the -nx/2 modes sit on the negative side only, kx[1] = eps is not odd -- P is not
 // Hermitian).  D: 4 arrays of (px/2 + 1) x py, x contiguous.
+template <bool NT>  // the four spectra (1.2 GB at 4096^2) by streaming stores
 __global__ void ps32_derivs_half_kernel(const double2* __restrict__ wf,
                                         const double* __restrict__ kx, double2* __restrict__ D,
                                         int nx, int ny, int px, int py, double sc, double sd) {
@@ -355,7 +356,7 @@ __global__ void ps32_derivs_half_kernel(const double2* __restrict__ wf,
       }
     }
 #pragma unroll
-    for (int q = 0; q < 4; ++q) D[q * nh + t] = acc[q];
+    for (int q = 0; q < 4; ++q) store_stream<NT>(D + q * nh + t, acc[q]);
   }
 }
 
@@ -582,8 +583,12 @@ struct cfdj_spec {
     if (real32) {
       const double sc = (double)px * py, sd = (double)nx * ny;
       const size_t nhp = (size_t)(px / 2 + 1) * py;
-      hipLaunchKernelGGL(ps32_derivs_half_kernel, dim3(grid_for(nhp)), dim3(256), 0, stream, wf,
-                         kx, X, nx, ny, px, py, sc, sd);
+      if (stream_loads)
+        hipLaunchKernelGGL(ps32_derivs_half_kernel<true>, dim3(grid_for(nhp)), dim3(256), 0,
+                           stream, wf, kx, X, nx, ny, px, py, sc, sd);
+      else
+        hipLaunchKernelGGL(ps32_derivs_half_kernel<false>, dim3(grid_for(nhp)), dim3(256), 0,
+                           stream, wf, kx, X, nx, ny, px, py, sc, sd);
       CFDJ_HIP(hipGetLastError());
       plans.exec(inv_r, X, R);
       product_real(gb, 1.0 / sc);
