@@ -213,6 +213,7 @@ struct FusedPoissonArgs {
   int ncu;              // compute units (persistent grid size)
   int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
   bool stream;          // pass 0: the input rows by streaming loads (load_stream)
+  bool stream_out;      // pass 2 (small-item kernel): the output rows by streaming stores
 };
 bool fused_poisson_supported(int nx, int ny, int rows);
 bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)

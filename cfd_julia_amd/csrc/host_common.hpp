@@ -288,7 +288,7 @@ struct Fused {
     a.recip = sym.kind == kSymbolDirichletExt;
     a.ncu = ncu;
     a.mmax = 0;
-    a.stream = stream_loads_pay((size_t)nx * rows * sizeof(double));
+    a.stream = a.stream_out = stream_loads_pay((size_t)nx * rows * sizeof(double));
     return a;
   }
   FusedPoissonArgs args(const Symbol& sym, const double* f, double* s, double2* H,
