@@ -129,7 +129,7 @@ struct StageCoef {
 // One slab of rows [0, ny) (local), pitch nx, x contiguous.  Row -1 / row ny are read
 // from the lo / hi ghost rows (on one GPU: the periodic wrap rows of the same array).
 struct StageParams {
-  bool stream = false;  // omega^n by streaming loads (load_stream)
+  bool stream = false;  // omega^n by streaming loads; marching kernel: the output by streaming stores
   const double* w;     // stencil input omega_s
   const double* w_lo;
   const double* w_hi;
