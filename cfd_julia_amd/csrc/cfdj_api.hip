@@ -400,6 +400,7 @@ struct cfdj_vm {
   void poisson_schur(const std::vector<const double*>& src, bool neg) {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
+    const bool col0_direct = fused_rows_take_col0(nx, rows);
     auto schur_args = [&](const Slab& s) {
       SchurArgs sa = schur.args(s.X, T, s.rank, out_scale, ny);
       sa.tile8 = 1;
@@ -427,6 +428,8 @@ struct cfdj_vm {
       a.push_back(fused.args(sym, src[i], slabs[i].psi, slabs[i].X, slabs[i].X, rows,
                              slabs[i].rank, nranks, neg));
       a.back().tile8 = 1;  // 8-mode tiles: whole-line row writes, shared column reads
+      // column m = 0 (packed DC / Nyquist) straight to and from the gathered column G
+      if (col0_direct) a.back().col0 = G + slabs[i].row0;
     }
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_FWD);
@@ -435,7 +438,8 @@ struct cfdj_vm {
     }
     // column m = 0 (packed DC / Nyquist) of the tiled spectrum: element j at 8 j
     tbegin(CFDJ_K_COMM);
-    for (auto& s : slabs) launch_strided_copy(G + s.row0, 1, s.X, 8, rows, stream);
+    if (!col0_direct)
+      for (auto& s : slabs) launch_strided_copy(G + s.row0, 1, s.X, 8, rows, stream);
     const bool aside = gather_on_side && mode == Mode::Rccl;
     if (aside) {
       CFDJ_HIP(hipEventRecord(ev_g, stream));
@@ -492,7 +496,8 @@ struct cfdj_vm {
       tend();
     }
     tbegin(CFDJ_K_COMM);
-    for (auto& s : slabs) launch_strided_copy(s.X, 8, G + s.row0, 1, rows, stream);
+    if (!col0_direct)
+      for (auto& s : slabs) launch_strided_copy(s.X, 8, G + s.row0, 1, rows, stream);
     tend();
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_INV);

@@ -211,11 +211,15 @@ struct FusedPoissonArgs {
   bool neg;
   bool recip;           // see DivideParams::recip
   int ncu;              // compute units (persistent grid size)
+  double2* col0;        // row passes, 8-mode tiles, where fused_rows_take_col0(): the packed
+                        // column 0 as a dense array [rows] -- written (also) by pass 0, read
+                        // (instead of H's column 0) by pass 2; null: H only
   int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
   bool stream;          // pass 0: the input rows by streaming loads (load_stream)
   bool stream_out;      // pass 2 (small-item kernel): the output rows by streaming stores
 };
 bool fused_poisson_supported(int nx, int ny, int rows);
+bool fused_rows_take_col0(int nx, int rows);
 bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);
 

@@ -288,6 +288,7 @@ struct Fused {
     a.recip = sym.kind == kSymbolDirichletExt;
     a.ncu = ncu;
     a.mmax = 0;
+    a.col0 = nullptr;
     a.stream = a.stream_out = stream_loads_pay((size_t)nx * rows * sizeof(double));
     return a;
   }

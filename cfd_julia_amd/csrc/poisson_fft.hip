@@ -23,6 +23,8 @@
 // contraction is allowed here: the FFT is not bit-comparable to FFTW / pocketfft anyway
 // (tolerance 1e-12 relative on psi, tests/test_gpu_parity.py).
 #pragma clang fp contract(fast)
+#include <type_traits>
+
 #include "fft_lds.hpp"
 
 namespace cfdj {
@@ -529,10 +531,13 @@ constexpr int rows_np_xr() {
 // but written the plain way its dirty lines sit in the caches while that kernel streams four
 // other arrays through them: stage kernels 87 -> 83 us, this pass 49 -> 47 (0.742 -> 0.727 ms
 // per step).  Chosen like the streaming loads: only where the fields outgrow the caches.
-template <int L, int XR, bool TILE, bool BAND = false, bool NTS = false>
+// COL0 (y-slab path): the packed column 0 comes from the dense array col0[row] (where the
+// gathered column's solve leaves it) instead of the spectrum.
+template <int L, int XR, bool TILE, bool BAND = false, bool NTS = false, bool COL0 = false>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
-    const double2* __restrict__ twL_, const double2* __restrict__ twN_, int mmax) {
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_, int mmax,
+    const double2* __restrict__ col0) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -559,6 +564,8 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     double2 Xm = make_double2(0.0, 0.0), Xq = Xm;
     if (!BAND || m <= mmax) Xm = base[(unsigned)sidx<TILE>(m, qq, M)];
     if (!BAND || mq <= mmax) Xq = base[(unsigned)sidx<TILE>(mq, qq, M)];
+    if constexpr (COL0)
+      if (z0) Xm = col0[y0 + qq];
     const double2 Xp = cconj(Xq);
     const double2 S = cadd(Xm, Xp);
     const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
@@ -600,10 +607,13 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
 // four workgroups per CU), used with the 8-mode-tile layout of the y-slab path, where one
 // row's modes are whole 128-B lines; in the column-major layout a small item's column
 // segments are too short to write (see above) and the persistent kernel stays.
-template <int L, int XR, bool TILE, bool NT>
+// COL0 (y-slab path): the packed column 0 goes to the dense array col0[row] as well, the
+// send buffer of that column's all-gather.
+template <int L, int XR, bool TILE, bool NT, bool COL0 = false>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
-    const double2* __restrict__ twL_, const double2* __restrict__ twN_) {
+    const double2* __restrict__ twL_, const double2* __restrict__ twN_,
+    double2* __restrict__ col0) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -671,6 +681,7 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     if (z0) {  // slot 0 = X[0] + i X[L]; X[L/2] = conj(Z[L/2])
       o1 = make_double2(Zm[i].x + Zm[i].y, Zm[i].x - Zm[i].y);
       o2 = Zc;
+      if constexpr (COL0) col0[y0 + qq] = o1;
     }
     hb[(unsigned)sidx<TILE>(m, qq, M)] = o1;
     hb[(unsigned)sidx<TILE>(mp, qq, M)] = o2;
@@ -697,18 +708,26 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
     if (a.tile8) {
       constexpr int XR = rows_np_xr<L, true>();
       if (a.rows % XR == 0) {
-        if (pass == 0 && a.stream)
-          hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, true>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.f, a.H, a.rows, a.twL, a.twN);
-        else if (pass == 0)
-          hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, false>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.f, a.H, a.rows, a.twL, a.twN);
-        else if (a.stream_out)
-          hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true, false, true>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0);
-        else
-          hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0);
+        const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
+        if (pass == 0) {
+          auto fwd = [&](auto nt, auto c0) {
+            hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, nt.value, c0.value>), grid, block,
+                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0);
+          };
+          using T = std::true_type;
+          using F = std::false_type;
+          if (a.stream) a.col0 ? fwd(T{}, T{}) : fwd(T{}, F{});
+          else a.col0 ? fwd(F{}, T{}) : fwd(F{}, F{});
+        } else {
+          auto inv = [&](auto nts, auto c0) {
+            hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true, false, nts.value, c0.value>), grid,
+                               block, 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, a.col0);
+          };
+          using T = std::true_type;
+          using F = std::false_type;
+          if (a.stream_out) a.col0 ? inv(T{}, T{}) : inv(T{}, F{});
+          else a.col0 ? inv(F{}, T{}) : inv(F{}, F{});
+        }
         return;
       }
     } else if (pass != 0 && L <= 2048) {
@@ -717,18 +736,19 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
         if (a.mmax > 0)  // (the spectral solvers' batches: plain stores measured as fast)
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false, true>), dim3(a.rows / XR),
                              dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN,
-                             a.mmax);
+                             a.mmax, nullptr);
         else if (a.stream_out)
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false, false, true>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0);
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, nullptr);
         else
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0);
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, nullptr);
         return;
       }
     }
   }
 #endif
+  if (a.col0) throw Error{CFDJ_ERR_ARG, "fused Poisson: dense column 0 unsupported here"};
   if (pass == 0) launch_rows_dir<L, true>(pass, a, st);
   else launch_rows_dir<L, false>(pass, a, st);
 }
@@ -783,6 +803,11 @@ constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 // pass's rows per work item (<= 8).
 bool fused_rows_supported(int nx, int rows) {
   return pow2(nx) && nx >= 1024 && nx <= 16384 && rows >= 8 && rows % 8 == 0;
+}
+
+// Whether the row passes of the 8-mode-tile layout take FusedPoissonArgs::col0.
+bool fused_rows_take_col0(int nx, int rows) {
+  return CFDJ_ROWS_INV_NP > 0 && fused_rows_supported(nx, rows) && nx <= 8192;
 }
 
 bool fused_poisson_supported(int nx, int ny, int rows) {
