@@ -418,9 +418,11 @@ struct cfdj_vm {
         if (idx < 3) s.cp_valid[idx] = true;
       }
       launch_colsum_row(s.colpart[idx], ncp, nx, s.cs8, stream);
-      FusedPoissonArgs ca = fused.args(sym, s.cs8, nullptr, s.cs, s.cs, 8, 0, 1, neg);
-      ca.tile8 = 1;
-      launch_fused_poisson_pass(0, ca, stream);
+      if (!col0_direct) {  // (else: a workgroup of the slab's own row pass below)
+        FusedPoissonArgs ca = fused.args(sym, s.cs8, nullptr, s.cs, s.cs, 8, 0, 1, neg);
+        ca.tile8 = 1;
+        launch_fused_poisson_pass(0, ca, stream);
+      }
       tend();
     }
     std::vector<FusedPoissonArgs> a;
@@ -429,7 +431,11 @@ struct cfdj_vm {
                              slabs[i].rank, nranks, neg));
       a.back().tile8 = 1;  // 8-mode tiles: whole-line row writes, shared column reads
       // column m = 0 (packed DC / Nyquist) straight to and from the gathered column G
-      if (col0_direct) a.back().col0 = G + slabs[i].row0;
+      if (col0_direct) {
+        a.back().col0 = G + slabs[i].row0;
+        a.back().fx = slabs[i].cs8;
+        a.back().Hx = slabs[i].cs;
+      }
     }
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_FWD);

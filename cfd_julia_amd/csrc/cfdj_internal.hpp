@@ -214,6 +214,8 @@ struct FusedPoissonArgs {
   double2* col0;        // row passes, 8-mode tiles, where fused_rows_take_col0(): the packed
                         // column 0 as a dense array [rows] -- written (also) by pass 0, read
                         // (instead of H's column 0) by pass 2; null: H only
+  const double* fx;     // pass 0 with col0: one more workgroup transforms the first rows of
+  double2* Hx;          // this 8-row array into this 8-row tiled spectrum (null: none)
   int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
   bool stream;          // pass 0: the input rows by streaming loads (load_stream)
   bool stream_out;      // pass 2 (small-item kernel): the output rows by streaming stores

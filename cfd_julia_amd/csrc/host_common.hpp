@@ -289,6 +289,8 @@ struct Fused {
     a.ncu = ncu;
     a.mmax = 0;
     a.col0 = nullptr;
+    a.fx = nullptr;
+    a.Hx = nullptr;
     a.stream = a.stream_out = stream_loads_pay((size_t)nx * rows * sizeof(double));
     return a;
   }

@@ -608,12 +608,14 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
 // row's modes are whole 128-B lines; in the column-major layout a small item's column
 // segments are too short to write (see above) and the persistent kernel stays.
 // COL0 (y-slab path): the packed column 0 goes to the dense array col0[row] as well, the
-// send buffer of that column's all-gather.
+// send buffer of that column's all-gather; and one workgroup beyond the slab's rows transforms
+// the first XR rows of the 8-row array fx (the slab's column-sum row and zeros) into the
+// 8-row tiled spectrum Hx, which would otherwise be a launch of its own between two others.
 template <int L, int XR, bool TILE, bool NT, bool COL0 = false>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_,
-    double2* __restrict__ col0) {
+    double2* __restrict__ col0, const double* __restrict__ fx, double2* __restrict__ Hx) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -621,7 +623,17 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
   const TwGlobal<2 * L> twN{twN_};
   const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
   double* buf = lds + q * P::PAD;
-  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  bool extra = false;
+  if constexpr (COL0) {
+    if (y0 >= M) {  // the one block whose index the (bijective) remap puts beyond the rows
+      extra = true;
+      f = fx;
+      H = Hx;
+      M = 8;
+      y0 = 0;
+    }
+  }
   double2 v[16];
   {
     const double2* z = reinterpret_cast<const double2*>(f) + (size_t)(y0 + q) * L;
@@ -681,7 +693,8 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     if (z0) {  // slot 0 = X[0] + i X[L]; X[L/2] = conj(Z[L/2])
       o1 = make_double2(Zm[i].x + Zm[i].y, Zm[i].x - Zm[i].y);
       o2 = Zc;
-      if constexpr (COL0) col0[y0 + qq] = o1;
+      if constexpr (COL0)
+        if (!extra) col0[y0 + qq] = o1;
     }
     hb[(unsigned)sidx<TILE>(m, qq, M)] = o1;
     hb[(unsigned)sidx<TILE>(mp, qq, M)] = o2;
@@ -710,9 +723,12 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
       if (a.rows % XR == 0) {
         const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
         if (pass == 0) {
+          if (a.fx && !(a.col0 && a.Hx))
+            throw Error{CFDJ_ERR_ARG, "fused Poisson: extra row without dense column 0"};
+          const dim3 gridx(a.rows / XR + (a.fx ? 1 : 0));
           auto fwd = [&](auto nt, auto c0) {
-            hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, nt.value, c0.value>), grid, block,
-                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0);
+            hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, nt.value, c0.value>), gridx, block,
+                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0, a.fx, a.Hx);
           };
           using T = std::true_type;
           using F = std::false_type;
@@ -748,7 +764,8 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
     }
   }
 #endif
-  if (a.col0) throw Error{CFDJ_ERR_ARG, "fused Poisson: dense column 0 unsupported here"};
+  if (a.col0 || a.fx)
+    throw Error{CFDJ_ERR_ARG, "fused Poisson: dense column 0 unsupported here"};
   if (pass == 0) launch_rows_dir<L, true>(pass, a, st);
   else launch_rows_dir<L, false>(pass, a, st);
 }
