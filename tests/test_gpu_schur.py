@@ -76,6 +76,27 @@ def test_gpu_schur_matches_transpose_path(cfdj):
     assert np.abs(out["schur"] - out["fused"]).max() < 1e-11
 
 
+def test_gpu_schur_16384_long_rows_vs_library_path(cfdj):
+    """Rows of 16384 reals are beyond the small-item row kernels: the persistent row kernels
+    run, and the packed column travels through strided copies.  psi of one right-hand side
+    against the library transposes' path on the same 8 slabs (no oracle at this size: the
+    NumPy solve would need minutes)."""
+    n, P = 16384, 8
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w = vo.to_ghosted(vo.vm_ic(n, n, x, y))
+    out = {}
+    for path in ("schur", "rocfft"):
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+            h.set_poisson(path)
+            assert h.poisson() == path
+            _, s = h.rhs(w)
+            out[path] = vo.from_ghosted(s)
+            del s
+    scale = np.abs(out["rocfft"]).max()
+    err = np.abs(out["schur"] - out["rocfft"]).max()
+    assert err <= 2e-12 * (n / 1024) ** 2 * scale, err / scale
+
+
 def test_gpu_schur_path_selection(cfdj):
     dx, dy, _, _ = vo.vm_grid(2048, 2048)
     with cfdj.VortexMerger(2048, 2048, dx, dy, 1000.0) as h:  # single GPU: no slabs
