@@ -1,4 +1,4 @@
-"""CPU oracle of the remaining §8(a) rows (TEST INFRASTRUCTURE ONLY):
+"""CPU oracle of the two small solvers beside the Navier-Stokes paths (TEST INFRASTRUCTURE ONLY):
 
   * 15_Poisson_Solver_Gauss_Seidel/gauss_seidel.jl:8-54 -- the reference's "Gauss-Seidel"
     is a Jacobi sweep (r = f - lap(u_old) everywhere, then u += r / dd), so a vectorised
