@@ -163,6 +163,23 @@ def test_gpu_vm_numerical_reference_signature(cfdj, tmp_path):
     assert np.array_equal(read_field(tmp_path / "vm1.txt", 64, 64), un)  # plotting.jl reader
 
 
+def test_gpu_vm_reference_default_run_to_t20(cfdj):
+    """vm.jl:93-105 as shipped: 128^2, dt = .01, tf = 20 (2000 RK3 steps), re = 1000.  The
+    merged vortex of the reference's figure (Python_Vectorized/field_fdm.png, colour bar to
+    about 0.74) and the oracle's field after the same 2000 steps."""
+    n, nt = 128, 2000
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    ref = vo.numerical(w0, nt, 0.01, dx, dy, 1000.0, workers=1)
+    with cfdj.VortexMerger(n, n, dx, dy, 1000.0) as h:
+        h.upload_interior(w0)
+        h.step(0.01, nt)
+        w = h.download_interior()
+    assert 0.72 < w.max() < 0.76, w.max()
+    # 2000 steps of a vortex merger amplify the transforms' round-off differences
+    assert np.abs(w - ref).max() < 1e-9, np.abs(w - ref).max()
+
+
 def test_gpu_tgv_known_answer(cfdj, golden):
     def stepper(w0, nt, dt, dx, dy, re):
         with cfdj.VortexMerger(w0.shape[0], w0.shape[1], dx, dy, re) as h:
