@@ -64,6 +64,29 @@ def test_gpu_cavity_steps_vs_oracle(lib, n, nt):
     assert np.allclose(rms, rms_ref, rtol=1e-8, atol=1e-16)
 
 
+def test_gpu_cavity_reference_default_run_to_steady_state(lib):
+    """lid_driven_cavity.jl:162-172 as shipped: 64^2, dt = .001, tf = 10 (10000 steps),
+    re = 100.  Against the oracle's fields after the same steps, and against the primary
+    vortex of the literature's Re = 100 cavity (Ghia, Ghia & Shin 1982: psi = -0.1034 at
+    (0.6172, 0.7344)), which a 64^2 second-order solution meets within a percent."""
+    from cfd_julia_amd import cavity
+
+    n, nt, dt = 64, 10000, 0.001
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    wn = np.zeros((n + 1, n + 1), order="F")
+    sn = np.zeros((n + 1, n + 1), order="F")
+    rms = np.zeros(nt)
+    cavity.numerical(n, n, nt, dx, dy, dt, 100.0, wn, sn, rms)
+    i, j = np.unravel_index(np.abs(sn).argmax(), sn.shape)
+    assert abs(sn[i, j] + 0.1034) < 0.001, sn[i, j]
+    assert abs(i * dx - 0.6172) <= dx and abs(j * dy - 0.7344) <= dy, (i, j)
+    assert rms[-1] < 1e-6  # steady
+    w_ref, s_ref, rms_ref = co.cavity_numerical(n, n, nt, dt, 100.0)
+    assert np.abs(sn - s_ref).max() < 1e-11
+    assert np.abs(wn - w_ref).max() < 1e-9 * np.abs(w_ref).max()
+    assert np.allclose(rms, rms_ref, rtol=1e-6, atol=1e-14)
+
+
 @pytest.mark.parametrize("nx,ny", [(512, 64), (1024, 256), (1536, 34), (4096, 16)])
 def test_gpu_cavity_row_group_stage_matches_separate_kernels(lib, monkeypatch, nx, ny):
     """The fused row-group stage + wall-vorticity kernel (nx a multiple of 512, ny even) and

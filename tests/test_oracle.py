@@ -122,6 +122,20 @@ def test_vortex_merger_peak_matches_reference_figure():
     assert 0.72 < w.max() < 0.76
 
 
+def test_cavity_oracle_default_run_matches_literature_vortex():
+    # lid_driven_cavity.jl:162-172 as shipped (64^2, dt = .001, 10000 steps, re = 100); the
+    # reference holds no number for it, the literature does: Ghia, Ghia & Shin (1982), Re = 100,
+    # primary vortex psi = -0.1034 at (0.6172, 0.7344)
+    from oracle import cavity_oracle as co
+
+    n = 64
+    w, s, rms = co.cavity_numerical(n, n, 10000, 0.001, 100.0)
+    i, j = np.unravel_index(np.abs(s).argmax(), s.shape)
+    assert abs(s[i, j] + 0.1034) < 0.001
+    assert abs(i / n - 0.6172) <= 1 / n and abs(j / n - 0.7344) <= 1 / n
+    assert rms[-1] < 1e-6
+
+
 def test_cpu_mirror_modules_import():
     # the host mirrors import without a GPU (compute raises CfdjError, never a CPU path)
     from cfd_julia_amd import common, fft_p, fft_s, vm  # noqa: F401
