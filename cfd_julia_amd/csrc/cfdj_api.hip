@@ -396,7 +396,8 @@ struct cfdj_vm {
 
   // y-slabs without a transpose (schur.hip): row r2c -> interior traces -> all-gather of
   // 4 numbers per x-mode -> separator solve + interior solve -> row c2r.  The packed
-  // DC / Nyquist column is gathered and solved with the reference symbol by rocFFT.
+  // DC / Nyquist column is gathered and solved with the reference symbol: by the single-GPU
+  // column kernel for columns of up to 8192, by library transforms beyond.
   void poisson_schur(const std::vector<const double*>& src, bool neg) {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
@@ -480,20 +481,29 @@ struct cfdj_vm {
     // gathered traces only
     if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_g2, 0));
     tbegin(CFDJ_K_DIVIDE);
-    plans.exec(g_fwd, G, nullptr);
-    PackedDivParams pd;
-    pd.Z = G;
-    pd.cx = sym.cx;
-    pd.cy = sym.cy;
-    pd.aa = sym.aa;
-    pd.bb = sym.bb;
-    pd.cc = sym.cc;
-    pd.scale = sym.scale;
-    pd.L = L;
-    pd.ny = ny;
-    pd.neg = neg;
-    launch_packed_divide(pd, stream);
-    plans.exec(g_inv, G, nullptr);
+    if (fused_poisson_supported(nx, ny, ny)) {
+      // the gathered column is column 0 of a one-column spectrum: the single-GPU column
+      // pass (forward FFT, packed divide, inverse FFT in one workgroup)
+      FusedPoissonArgs ga = fused.args(sym, nullptr, nullptr, G, G, ny, 0, 1, neg);
+      ga.kb = 1;
+      ga.seg = (unsigned)ny;
+      launch_fused_poisson_pass(1, ga, stream);
+    } else {
+      plans.exec(g_fwd, G, nullptr);
+      PackedDivParams pd;
+      pd.Z = G;
+      pd.cx = sym.cx;
+      pd.cy = sym.cy;
+      pd.aa = sym.aa;
+      pd.bb = sym.bb;
+      pd.cc = sym.cc;
+      pd.scale = sym.scale;
+      pd.L = L;
+      pd.ny = ny;
+      pd.neg = neg;
+      launch_packed_divide(pd, stream);
+      plans.exec(g_inv, G, nullptr);
+    }
     tend();
     if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_t2, 0));
     for (auto& s : slabs) {

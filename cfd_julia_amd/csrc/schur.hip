@@ -17,7 +17,9 @@
 //          solved directly in 32-row chunks + a reduced interface system -- and writes
 //          psi-hat (plus the constant-mode correction) in place.
 // The x-modes 0 and nx/2 (packed in column 0) are solved separately: the column is gathered
-// and FFT'd along y with the reference symbol (packed_divide_kernel).
+// and solved along y with the reference symbol (columns of up to 8192: the single-GPU column
+// pass of poisson_fft.hip on that one column; longer: library transforms around
+// packed_divide_kernel).
 // Host-side tables (long double): the circulant inverse, corr, the Green's function of the
 // trace pass, the chunk / interface pivots and homogeneous solutions -- host_common.hpp.
 #pragma clang fp contract(fast)
