@@ -64,6 +64,7 @@ SIGNATURES = {
                                       C.c_double, C.c_int, C.c_int, C.c_int, C.c_char_p,
                                       C.POINTER(_vp)]),
     "cfdj_comm_unique_id": (C.c_int, [C.c_char_p]),
+    "cfdj_vm_comm_ranks": (C.c_int, [_vp, _ip]),
     "cfdj_vm_create_virtual": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double,
                                          C.c_double, C.c_double, C.c_int, C.c_int,
                                          C.POINTER(_vp)]),
@@ -81,6 +82,7 @@ SIGNATURES = {
     "cfdj_vm_field_device": (C.c_int, [_vp, C.POINTER(_vp)]),
     "cfdj_vm_slab": (C.c_int, [_vp, _ip, _ip]),
     "cfdj_vm_set_rows_per_wave": (C.c_int, [_vp, C.c_int]),
+    "cfdj_vm_stage_kernel": (C.c_int, [_vp, _ip]),
     "cfdj_vm_set_graph": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_set_poisson": (C.c_int, [_vp, C.c_int]),
     "cfdj_vm_get_poisson": (C.c_int, [_vp]),

@@ -1069,6 +1069,14 @@ int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double 
   });
 }
 
+int cfdj_vm_comm_ranks(cfdj_vm* h, int* ranks) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && ranks, "NULL argument");
+    *ranks = 0;
+    if (h->comm) CFDJ_NCCL(ncclCommCount(h->comm, ranks));
+  });
+}
+
 int cfdj_vm_upload(cfdj_vm* h, const double* w, long ldw) {
   return guard([&] {
     CFDJ_REQUIRE(h && w, "NULL argument");
@@ -1256,6 +1264,16 @@ int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows) {
     h->stage_march = true;
     if (h->use_schur) h->alloc_colparts();  // partial blocks follow the wave row ranges
     h->invalidate_graph();
+  });
+}
+
+int cfdj_vm_stage_kernel(cfdj_vm* h, int* row_group) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && row_group, "NULL argument");
+    Slab& s = h->slabs[0];
+    StageParams p = h->stage_params(s, s.wn, s.wn, s.wa, 0.0);
+    if (h->use_schur) p.colpart = s.colpart[1];
+    *row_group = stage_runs_row_group(p) ? 1 : 0;
   });
 }
 

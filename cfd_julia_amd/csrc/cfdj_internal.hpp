@@ -147,6 +147,9 @@ struct StageParams {
 };
 
 void launch_stage(int stage, const StageParams& p, hipStream_t st);
+// Which kernel launch_stage picks for these parameters: the row-group one (true) or the
+// marching one.
+bool stage_runs_row_group(const StageParams& p);
 // Column sums of a slab field in the stage kernel's partial layout (rows_per_wave blocks):
 // colpart[b][x] = sum of f[y][x] over rows y of block b (fields not written by a stage).
 void launch_colpart(const double* f, int nx, int rows, int rpw, double* colpart,

@@ -339,6 +339,8 @@ static bool stage_tile_ok(const StageParams& p) {
          p.ycount % kTileRows == 0 && p.ycount > 0;
 }
 
+bool stage_runs_row_group(const StageParams& p) { return stage_tile_ok(p); }
+
 void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
     throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};

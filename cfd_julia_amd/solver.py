@@ -110,6 +110,12 @@ class VortexMerger:
         check(_lib.load().cfdj_comm_unique_id(buf), "cfdj_comm_unique_id")
         return buf.raw
 
+    def comm_ranks(self) -> int:
+        """Ranks of the handle's RCCL communicator as RCCL reports them (0: none)."""
+        n = C.c_int()
+        check(_lib.load().cfdj_vm_comm_ranks(self._h, C.byref(n)), "cfdj_vm_comm_ranks")
+        return n.value
+
     # ---- data movement (reference ghosted layout) -----------------------------------
     def upload(self, w_ghosted):
         w = np.asfortranarray(w_ghosted, dtype=np.float64)
@@ -188,6 +194,12 @@ class VortexMerger:
     def set_rows_per_wave(self, rows):
         check(_lib.load().cfdj_vm_set_rows_per_wave(self._h, int(rows)),
               "cfdj_vm_set_rows_per_wave")
+
+    def stage_row_group(self) -> bool:
+        """True where a step launches the row-group stage kernel, False: the marching one."""
+        f = C.c_int()
+        check(_lib.load().cfdj_vm_stage_kernel(self._h, C.byref(f)), "cfdj_vm_stage_kernel")
+        return bool(f.value)
 
     def set_graph(self, enable=True):
         check(_lib.load().cfdj_vm_set_graph(self._h, int(bool(enable))), "cfdj_vm_set_graph")

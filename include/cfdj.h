@@ -36,9 +36,10 @@ extern "C" {
 
 /* Kernel-category indices for cfdj_vm_timing(). */
 #define CFDJ_K_STAGE 0    /* fused Arakawa Jacobian + 5-pt Laplacian + RK3 stage kernel */
-#define CFDJ_K_FFT_FWD 1  /* rocFFT D2Z (forward real 2D / row transforms) */
-#define CFDJ_K_DIVIDE 2   /* spectral divide by the FD symbol (Common.jl:119-121) */
-#define CFDJ_K_FFT_INV 3  /* rocFFT Z2D (inverse) */
+#define CFDJ_K_FFT_FWD 1  /* forward transforms: hand-written row r2c pass, or rocFFT D2Z */
+#define CFDJ_K_DIVIDE 2   /* column pass (FFT + divide by the FD symbol, Common.jl:119-121, +
+                             inverse FFT), the substructured y-solve, or the divide kernel */
+#define CFDJ_K_FFT_INV 3  /* inverse transforms: hand-written row c2r pass, or rocFFT Z2D */
 #define CFDJ_K_COMM 4     /* halo exchange + FFT transposes (multi-GPU only) */
 #define CFDJ_K_COUNT 5
 
@@ -114,6 +115,9 @@ int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double 
                         int device, int rank, int nranks, const void* nccl_id,
                         cfdj_vm** out);
 int cfdj_comm_unique_id(void* out128);
+/* Number of ranks of the handle's RCCL communicator as RCCL itself reports it
+ * (ncclCommCount); 0 for handles without a communicator (single-GPU, virtual slabs). */
+int cfdj_vm_comm_ranks(cfdj_vm* h, int* ranks);
 /* Virtual-rank variant for testing the slab decomposition on ONE GPU: nranks slabs,
  * halo exchange and FFT transposes by device copies in one process. */
 int cfdj_vm_create_virtual(int nx, int ny, double dx, double dy, double re, double eps,
@@ -170,6 +174,8 @@ int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows);
  * (nx a multiple of 512, even row count, no column partial sums) and the marching kernel,
  * with a rows-per-wavefront default chosen per size, elsewhere.  Results are bit-identical. */
 int cfdj_vm_set_rows_per_wave(cfdj_vm* h, int rows);
+/* The stage kernel a step of this handle launches: 1 = row-group kernel, 0 = marching. */
+int cfdj_vm_stage_kernel(cfdj_vm* h, int* row_group);
 /* Replay cfdj_vm_step's kernel sequence from a captured HIP graph (default on; used on
  * single-GPU handles with the fused Poisson path, others launch eagerly). */
 int cfdj_vm_set_graph(cfdj_vm* h, int enable);
