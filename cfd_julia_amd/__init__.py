@@ -6,6 +6,10 @@ Modules mirror the reference files they replace:
   common  -- Common.jl (fps, vm_rhs, vm_ic, compute_l2norm*)
   vm      -- 19_NS2D_Vortex_Merger/vm.jl (numerical, main)
   fft_p   -- 12_Poisson_Solver_FFT/fft_p.jl (ps_fft, main)
+  fft_s   -- 13_Poisson_Solver_FFT_Spectral/fft_s.jl (ps_spectral)
+  fft_d   -- 14_Poisson_Solver_FST/fft_d.jl (ps_fst, main)
+  cavity  -- 18_NS2D_Lid_Driven_Cavity/lid_driven_cavity.jl (fps_sine, numerical, main)
+  mg      -- 17_Poisson_Solver_Multigrid/mg_N.jl and mg.jl
   solver  -- handle objects (VortexMerger, PoissonFFT)
   dist    -- one-process-per-GPU y-slab driver over RCCL
 """

@@ -55,6 +55,7 @@ SIGNATURES = {
     "cfdj_fps_solve": (C.c_int, [_vp, _dp, C.c_long, _dp, C.c_long]),
     "cfdj_fps_solve_device": (C.c_int, [_vp, _vp, _vp]),
     "cfdj_fps_solve_device_noalloc": (C.c_int, [_vp, _vp, _vp]),
+    "cfdj_fps_stream": (C.c_int, [_vp, C.POINTER(_vp)]),
     "cfdj_fps_destroy": (None, [_vp]),
     "cfdj_fps": (C.c_int, [C.c_int, C.c_int, C.c_double, C.c_double, C.c_double, _dp,
                            C.c_long, _dp, C.c_long]),

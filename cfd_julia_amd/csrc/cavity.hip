@@ -4,10 +4,11 @@
 // Fields are (nx+1) x (ny+1) node arrays, x contiguous, pitch nx+2 (even: 16-B rows).
 // Stencil / boundary / multigrid kernels keep the reference's expression order and are
 // compiled without FMA contraction (Makefile), so given the same inputs they reproduce the
-// CPU oracle bit for bit.  The DST-I Poisson (fps_sine) runs as the periodic FFT Poisson
-// of the odd-odd extension onto a (2nx) x (2ny) grid with the reference's iden multiplier
-// (host_common.hpp, kSymbolDirichletExt), so the C4 cavity at 2048^2 uses the fused 3-pass
-// FFT kernels on a 4096^2 extension.
+// CPU oracle bit for bit.  The DST-I Poisson (fps_sine) is a real DST-I on the (nx-1) x
+// (ny-1) interior in three passes (dst_poisson.hip) with the reference's iden multiplier;
+// CFDJ_CAVITY_EXT=1 (and grids the DST kernels do not cover) run it as the periodic FFT
+// Poisson of the odd-odd extension onto a (2nx) x (2ny) grid instead (host_common.hpp,
+// kSymbolDirichletExt).
 #include "host_common.hpp"
 
 namespace cfdj {
@@ -1631,12 +1632,22 @@ int cfdj_cavity_rhs(cfdj_cavity* h, const double* w, long ldw, const double* s, 
     CFDJ_REQUIRE(h && w && s && r, "NULL argument");
     CFDJ_REQUIRE(ldw >= h->nx + 1 && lds >= h->nx + 1 && ldr >= h->nx + 1, "bad ld");
     select_device(h->device);
-    copy_in(h->wa, h->P, w, ldw, h->nx, h->ny, h->stream);
-    copy_in(h->sn, h->P, s, lds, h->nx, h->ny, h->stream);
-    CFDJ_HIP(hipMemsetAsync(h->wb, 0, h->field() * sizeof(double), h->stream));
-    h->stage(0, h->wa, h->wb, 0.0);
-    copy_out(r, ldr, h->wb, h->P, h->nx, h->ny, h->stream);
-    CFDJ_HIP(hipStreamSynchronize(h->stream));
+    // the caller's psi goes to a buffer of its own: the handle's two psi buffers (and their
+    // common boundary values, which cfdj_cavity_step relies on) stay as they are
+    double* psi = dalloc<double>(h->field());
+    try {
+      copy_in(h->wa, h->P, w, ldw, h->nx, h->ny, h->stream);
+      copy_in(psi, h->P, s, lds, h->nx, h->ny, h->stream);
+      CFDJ_HIP(hipMemsetAsync(h->wb, 0, h->field() * sizeof(double), h->stream));
+      h->stage(0, h->wa, h->wb, 0.0, psi);
+      copy_out(r, ldr, h->wb, h->P, h->nx, h->ny, h->stream);
+      CFDJ_HIP(hipStreamSynchronize(h->stream));
+    } catch (...) {
+      (void)hipStreamSynchronize(h->stream);
+      dfree(psi);
+      throw;
+    }
+    dfree(psi);
   });
 }
 

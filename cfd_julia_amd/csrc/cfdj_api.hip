@@ -149,6 +149,11 @@ struct cfdj_vm {
   double2* T = nullptr;
   int ncp = 0;  // column-sum partial rows (blocks of rows_per_wave rows)
   double2* G = nullptr;
+  // virtual slabs with the side-stream schedule: what a rank contributes to an all-gather
+  // goes to these staging copies first and reaches G / T only through the side stream's
+  // copy (the stand-in for the collective), so a consumer that does not wait for it reads
+  // the previous solve's values, as it would on real ranks
+  double2 *Gs = nullptr, *Ts = nullptr;
   rocfft_plan g_fwd = nullptr, g_inv = nullptr;
   ncclComm_t comm = nullptr;
   // RCCL slabs: halo exchanges on a side stream, overlapped with the Poisson passes (omega
@@ -251,9 +256,9 @@ struct cfdj_vm {
   template <class Pick>
   void alltoall(Pick pick, size_t count) {
     tbegin(CFDJ_K_COMM);
+    comm_order();
     if (mode == Mode::Rccl) {
       Slab& s = slabs[0];
-      comm_order();
       CFDJ_NCCL(ncclAllToAll(pick(s, true), pick(s, false), 2 * count, ncclDouble, comm,
                              stream));
     } else {
@@ -296,8 +301,8 @@ struct cfdj_vm {
         double* lo = slabs[p].ghost + (size_t)(off + 0) * nx;
         double* hi = slabs[p].ghost + (size_t)(off + 1) * nx;
         CFDJ_HIP(hipMemcpyAsync(lo, src[prev] + (size_t)(slabs[prev].rows - 1) * nx, bytes,
-                                hipMemcpyDeviceToDevice, stream));
-        CFDJ_HIP(hipMemcpyAsync(hi, src[next], bytes, hipMemcpyDeviceToDevice, stream));
+                                hipMemcpyDeviceToDevice, hs));
+        CFDJ_HIP(hipMemcpyAsync(hi, src[next], bytes, hipMemcpyDeviceToDevice, hs));
       }
     }
     tend();
@@ -402,8 +407,12 @@ struct cfdj_vm {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
     const bool col0_direct = fused_rows_take_col0(nx, rows);
-    auto schur_args = [&](const Slab& s) {
-      SchurArgs sa = schur.args(s.X, T, s.rank, out_scale, ny);
+    // the exchanges on the side stream (RCCL ranks, or virtual slabs rehearsing that schedule
+    // with staged device copies)
+    const bool aside = gather_on_side && side != nullptr;
+    const bool staged = aside && mode == Mode::Virtual;
+    auto schur_args = [&](const Slab& s, bool trace_pass) {
+      SchurArgs sa = schur.args(s.X, staged && trace_pass ? Ts : T, s.rank, out_scale, ny);
       sa.tile8 = 1;
       sa.cs = s.cs;
       return sa;
@@ -438,20 +447,26 @@ struct cfdj_vm {
         a.back().Hx = slabs[i].cs;
       }
     }
-    for (auto& ai : a) {
+    double2* Gw = staged ? Gs : G;  // where the ranks put their pieces of the packed column
+    for (size_t i = 0; i < a.size(); ++i) {
+      FusedPoissonArgs a0 = a[i];
+      if (col0_direct) a0.col0 = Gw + slabs[i].row0;
       tbegin(CFDJ_K_FFT_FWD);
-      launch_fused_poisson_pass(0, ai, stream);
+      launch_fused_poisson_pass(0, a0, stream);
       tend();
     }
     // column m = 0 (packed DC / Nyquist) of the tiled spectrum: element j at 8 j
     tbegin(CFDJ_K_COMM);
     if (!col0_direct)
-      for (auto& s : slabs) launch_strided_copy(G + s.row0, 1, s.X, 8, rows, stream);
-    const bool aside = gather_on_side && mode == Mode::Rccl;
+      for (auto& s : slabs) launch_strided_copy(Gw + s.row0, 1, s.X, 8, rows, stream);
     if (aside) {
       CFDJ_HIP(hipEventRecord(ev_g, stream));
       CFDJ_HIP(hipStreamWaitEvent(side, ev_g, 0));
-      CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, side));
+      if (mode == Mode::Rccl)
+        CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, side));
+      else
+        CFDJ_HIP(hipMemcpyAsync(G, Gs, (size_t)ny * sizeof(double2), hipMemcpyDeviceToDevice,
+                                side));
       CFDJ_HIP(hipEventRecord(ev_g2, side));
     } else if (mode == Mode::Rccl) {
       comm_order();
@@ -460,10 +475,10 @@ struct cfdj_vm {
     tend();
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
-      launch_schur_pass(0, schur_args(s), stream);
+      launch_schur_pass(0, schur_args(s, true), stream);
       tend();
     }
-    if (mode == Mode::Rccl) {
+    if (mode == Mode::Rccl || staged) {
       tbegin(CFDJ_K_COMM);
       const size_t cnt = (size_t)L * 4 * 2;  // doubles per rank
       hipStream_t cs = stream;
@@ -472,8 +487,12 @@ struct cfdj_vm {
         CFDJ_HIP(hipStreamWaitEvent(side, ev_t, 0));
         cs = side;
       }
-      CFDJ_NCCL(ncclAllGather(reinterpret_cast<double*>(T) + (size_t)rank * cnt, T, cnt,
-                              ncclDouble, comm, cs));
+      if (mode == Mode::Rccl)
+        CFDJ_NCCL(ncclAllGather(reinterpret_cast<double*>(T) + (size_t)rank * cnt, T, cnt,
+                                ncclDouble, comm, cs));
+      else
+        CFDJ_HIP(hipMemcpyAsync(T, Ts, (size_t)nranks * cnt * sizeof(double),
+                                hipMemcpyDeviceToDevice, cs));
       if (aside) CFDJ_HIP(hipEventRecord(ev_t2, side));
       tend();
     }
@@ -508,7 +527,7 @@ struct cfdj_vm {
     if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_t2, 0));
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
-      launch_schur_pass(1, schur_args(s), stream);
+      launch_schur_pass(1, schur_args(s, false), stream);
       tend();
     }
     tbegin(CFDJ_K_COMM);
@@ -566,9 +585,9 @@ struct cfdj_vm {
     std::vector<const double*> src(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i)
       src[i] = st == 1 ? slabs[i].wn : st == 2 ? slabs[i].wa : slabs[i].wb;
-    if (mode == Mode::Rccl && side && !timing && rows % rows_per_wave == 0 &&
+    if (slab_mode() && side && !timing && rows % rows_per_wave == 0 &&
         rows >= 3 * rows_per_wave) {
-      stage_overlapped(st, dt, src[0]);
+      stage_overlapped(st, dt, src);
       return;
     }
     poisson(src, true);
@@ -593,19 +612,20 @@ struct cfdj_vm {
     }
   }
 
-  // The RCCL-slab stage with the halo exchanges on the side stream: omega halo during the
-  // Poisson passes, psi halo during the interior rows of the stage kernel; the first and
-  // last rows (which read the halo rows) run after it.
-  void stage_overlapped(int st, double dt, const double* src) {
-    Slab& s = slabs[0];
+  // The y-slab stage with the exchanges on the side stream: omega halo during the Poisson
+  // passes, psi halo during the interior rows of the stage kernel; the first and last rows
+  // (which read the halo rows) run after it.  RCCL ranks (one slab), and virtual slabs created
+  // with CFDJ_VIRTUAL_OVERLAP=1, which run the identical event schedule with device copies in
+  // place of the collectives.
+  void stage_overlapped(int st, double dt, const std::vector<const double*>& src) {
     CFDJ_HIP(hipEventRecord(ev_src, stream));
     CFDJ_HIP(hipStreamWaitEvent(side, ev_src, 0));
-    halo(false, {src}, side);
+    halo(false, src, side);
     CFDJ_HIP(hipEventRecord(ev_whalo, side));
     whalo_pending = true;
     gather_on_side = use_schur;
     try {
-      poisson({src}, true);
+      poisson(src, true);
     } catch (...) {
       gather_on_side = false;
       throw;
@@ -614,27 +634,36 @@ struct cfdj_vm {
     comm_order();  // paths without a collective on the main stream before the psi halo
     CFDJ_HIP(hipEventRecord(ev_psi, stream));
     CFDJ_HIP(hipStreamWaitEvent(side, ev_psi, 0));
-    halo(true, {s.psi}, side);
+    std::vector<const double*> ps(slabs.size());
+    for (size_t i = 0; i < slabs.size(); ++i) ps[i] = slabs[i].psi;
+    halo(true, ps, side);
     CFDJ_HIP(hipEventRecord(ev_shalo, side));
-    double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
-    StageParams p = stage_params(s, src, s.wn, out, dt);
-    if (use_schur) {
-      const int oi = st == 1 ? 1 : st == 2 ? 2 : 0;
-      p.colpart = s.colpart[oi];
-      s.cp_valid[oi] = true;
-    }
     // interior blocks first, then the first / last rows_per_wave rows (which read the halo
     // rows); block-aligned, so the column partials match the one-launch order
     const int rb = rows_per_wave;
-    p.y0 = rb;
-    p.ycount = rows - 2 * rb;
-    launch_stage(st, p, stream);
+    std::vector<StageParams> sp;
+    for (size_t i = 0; i < slabs.size(); ++i) {
+      Slab& s = slabs[i];
+      double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
+      StageParams p = stage_params(s, src[i], s.wn, out, dt);
+      if (use_schur) {
+        const int oi = st == 1 ? 1 : st == 2 ? 2 : 0;
+        p.colpart = s.colpart[oi];
+        s.cp_valid[oi] = true;
+      }
+      p.y0 = rb;
+      p.ycount = rows - 2 * rb;
+      launch_stage(st, p, stream);
+      sp.push_back(p);
+    }
     CFDJ_HIP(hipStreamWaitEvent(stream, ev_shalo, 0));
-    p.ycount = rb;
-    p.y0 = 0;
-    launch_stage(st, p, stream);
-    p.y0 = rows - rb;
-    launch_stage(st, p, stream);
+    for (StageParams& p : sp) {
+      p.ycount = rb;
+      p.y0 = 0;
+      launch_stage(st, p, stream);
+      p.y0 = rows - rb;
+      launch_stage(st, p, stream);
+    }
   }
 
   // `n` back-to-back launches of ONE kernel of the step between two events on the handle's
@@ -735,6 +764,13 @@ struct cfdj_vm {
     }
   }
 
+  // side stream (default priority) and the events that order it against the main stream
+  void create_side() {
+    CFDJ_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    for (hipEvent_t* e : {&ev_src, &ev_whalo, &ev_psi, &ev_shalo, &ev_g, &ev_g2, &ev_t, &ev_t2})
+      CFDJ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  }
+
   void init_buffers() {
     nxh = nx / 2 + 1;
     const int P = nranks;
@@ -816,6 +852,8 @@ struct cfdj_vm {
     schur.destroy();
     dfree(T);
     dfree(G);
+    dfree(Gs);
+    dfree(Ts);
     dfree(spec);
     dfree(gather);
     dfree(d_flag);
@@ -941,7 +979,9 @@ int cfdj_fps_create(int nx, int ny, double dx, double dy, double eps, int device
       h->fused.init(nx, ny);
       h->use_fused = true;
     }
-    h->static_spec = noalloc_scratch_init();  // set-up: the plan's device is current
+    // set-up, the plan's device current: only plans that can use the static scratch look its
+    // address up (a failing lookup must not break plans on the library-FFT path)
+    if (h->use_fused) h->static_spec = noalloc_scratch_init();
     *out = h.release();
   });
 }
@@ -992,6 +1032,13 @@ int cfdj_fps_solve_device_noalloc(cfdj_fps_plan* h, const double* f_dev, double*
   });
 }
 
+int cfdj_fps_stream(cfdj_fps_plan* h, void** hip_stream) {
+  return guard([&] {
+    CFDJ_REQUIRE(h && hip_stream, "NULL argument");
+    *hip_stream = static_cast<void*>(h->stream);
+  });
+}
+
 void cfdj_fps_destroy(cfdj_fps_plan* h) {
   if (!h) return;
   (void)guard([&] {
@@ -1025,7 +1072,19 @@ int cfdj_vm_create_virtual(int nx, int ny, double dx, double dy, double re, doub
   return guard([&] {
     CFDJ_REQUIRE(out != nullptr, "out is NULL");
     *out = nullptr;
-    *out = new_vm(nx, ny, dx, dy, re, eps, device, Mode::Virtual, nranks, 0);
+    std::unique_ptr<cfdj_vm> h(new_vm(nx, ny, dx, dy, re, eps, device, Mode::Virtual, nranks, 0));
+    // CFDJ_VIRTUAL_OVERLAP=1: the RCCL ranks' side-stream schedule (halo exchanges and the
+    // substructured solve's two gathers behind events) with staged device copies standing in
+    // for the collectives -- the event graph of the multi-GPU step on one GPU
+    const char* ov = std::getenv("CFDJ_VIRTUAL_OVERLAP");
+    if (ov && ov[0] == '1') {
+      h->create_side();
+      if (h->T) {
+        h->Ts = dalloc<double2>((size_t)nranks * (nx / 2) * 4);
+        h->Gs = dalloc<double2>((size_t)ny);
+      }
+    }
+    *out = h.release();
   });
 }
 
@@ -1059,12 +1118,7 @@ int cfdj_vm_create_dist(int nx, int ny, double dx, double dy, double re, double 
     CFDJ_NCCL(ncclCommInitRank(&h->comm, nranks, id, rank));
     // halo overlap (CFDJ_NO_OVERLAP=1: everything on one stream, for A/B runs)
     const char* no_ov = std::getenv("CFDJ_NO_OVERLAP");
-    if (!(no_ov && no_ov[0] == '1')) {
-      CFDJ_HIP(hipStreamCreateWithFlags(&h->side, hipStreamNonBlocking));
-      for (hipEvent_t* e : {&h->ev_src, &h->ev_whalo, &h->ev_psi, &h->ev_shalo, &h->ev_g,
-                            &h->ev_g2, &h->ev_t, &h->ev_t2})
-        CFDJ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
-    }
+    if (!(no_ov && no_ov[0] == '1')) h->create_side();
     *out = h.release();
   });
 }
@@ -1336,6 +1390,7 @@ int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path) {
     select_device(h->device);
     const bool f = resolve_fused(path, h->sym.nx, h->sym.ny, 1);
     if (f && !h->fused.ready()) h->fused.init(h->sym.nx, h->sym.ny);
+    if (f && !h->static_spec) h->static_spec = noalloc_scratch_init();
     h->use_fused = f;
   });
 }

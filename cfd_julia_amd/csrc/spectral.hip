@@ -440,14 +440,31 @@ __global__ void to_field_real_kernel(const double* __restrict__ R, double* __res
 }
 
 // Full spectrum (nx x ny, kx contiguous) <-> half spectrum ((nx/2 + 1) columns of ny, ky
-// contiguous) of a real field: the other half is conj(w_f(-kx, -ky)).
+// contiguous) of a real field: the other half is conj(w_f(-kx, -ky)).  The import keeps the
+// Hermitian part (w_f(k) + conj(w_f(-k))) / 2 of whatever it is given -- the part the
+// reference's jacobian() sees through real(ifft(.)) (hybrid.jl:103,115) -- so a spectrum
+// that is not that of a real field gives the same Jacobian here as on the full-spectrum path.
 __global__ void full_to_half_kernel(const double2* __restrict__ full, double2* __restrict__ hs,
                                     int nx, int ny) {
   const size_t n = (size_t)(nx / 2 + 1) * ny;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
        t += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(t / ny), k = (int)(t % ny);
-    hs[t] = full[(size_t)k * nx + m];
+    const double2 a = full[(size_t)k * nx + m];
+    const double2 b = full[(size_t)(k == 0 ? 0 : ny - k) * nx + (m == 0 ? 0 : nx - m)];
+    hs[t] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+  }
+}
+// The same projection on the full layout: out(k) = (full(k) + conj(full(-k))) / 2.
+__global__ void hermitian_part_kernel(const double2* __restrict__ full,
+                                      double2* __restrict__ out, int nx, int ny) {
+  const size_t n = (size_t)nx * ny;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+       t += (size_t)gridDim.x * blockDim.x) {
+    const int i = (int)(t % nx), j = (int)(t / nx);
+    const double2 a = full[t];
+    const double2 b = full[(size_t)(j == 0 ? 0 : ny - j) * nx + (i == 0 ? 0 : nx - i)];
+    out[t] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
   }
 }
 __global__ void half_to_full_kernel(const double2* __restrict__ hs, double2* __restrict__ full,
@@ -647,7 +664,16 @@ struct cfdj_spec {
       hipLaunchKernelGGL(full_to_half_kernel, dim3(grid_for(nh())), dim3(256), 0, stream, full,
                          dst, nx, ny);
       CFDJ_HIP(hipGetLastError());
+    } else if (kind != CFDJ_SPEC_PS32) {
+      // hybrid.jl:103,115 and pseudospectral_23_rule.jl:135-138 see w_f through real(ifft(.))
+      // of spectra whose multipliers are Hermitian (the 2/3 rule zeroes the Nyquist modes),
+      // i.e. its Hermitian part only; the real-field transforms here assume that symmetry
+      hipLaunchKernelGGL(hermitian_part_kernel, dim3(grid_for(n())), dim3(256), 0, stream, full,
+                         dst, nx, ny);
+      CFDJ_HIP(hipGetLastError());
     } else {
+      // 3/2 rule: the padded Nyquist modes enter with their own value (no mirror partner in
+      // the padded spectrum, pseudospectral_32_rule.jl:124-133): kept as given
       CFDJ_HIP(hipMemcpyAsync(dst, full, n() * sizeof(double2), hipMemcpyDeviceToDevice, stream));
     }
   }

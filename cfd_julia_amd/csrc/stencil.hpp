@@ -1,6 +1,7 @@
-// The vortex-merger RHS arithmetic shared by the stage kernels (vm_kernels.hip) and the
-// FFT-fused stage kernel (vm_fused.hip): Arakawa Jacobian + 5-point Laplacian
-// (Common.jl:148-181) and the SSP-RK3 stage combinations (vm.jl:28, 43-47, 62-66).
+// The vortex-merger RHS arithmetic shared by the marching and the row-group stage kernels
+// (vm_kernels.hip) and the spectral solvers' Arakawa kernel (spectral.hip): Arakawa Jacobian
+// + 5-point Laplacian (Common.jl:148-181) and the SSP-RK3 stage combinations (vm.jl:28,
+// 43-47, 62-66).
 //
 // Every function body pins `fp contract(off)`: the expressions are evaluated in the
 // reference's written order without FMA, so given the same streamfunction the output is

@@ -62,6 +62,12 @@ class PoissonFFT:
                                                         C.c_void_p(s_ptr)),
               "cfdj_fps_solve_device_noalloc")
 
+    def stream(self):
+        """The plan's hipStream_t (as an integer) the device solves are enqueued on."""
+        p = C.c_void_p()
+        check(_lib.load().cfdj_fps_stream(self._h, C.byref(p)), "cfdj_fps_stream")
+        return p.value
+
     def close(self):
         if getattr(self, "_h", None):
             _lib.load().cfdj_fps_destroy(self._h)

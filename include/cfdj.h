@@ -82,15 +82,20 @@ int cfdj_fps_solve(cfdj_fps_plan* h, const double* f, long ldf, double* s, long 
 /* Same, on device pointers (contiguous, pitch nx) on the handle's stream; no sync. */
 int cfdj_fps_solve_device(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
 /* No counterpart in the reference: cfdj_fps_solve_device for callers that cannot allocate
- * device memory (code under HIP graph capture, tight serving loops, harnesses that forbid
- * hipMalloc).  The half spectrum lives in a static device array of the library instead of
- * the plan's buffer; the call itself runs only the three hand-written FFT passes on the
- * plan's stream (no hipMalloc / hipFree / rocFFT), no sync.  Limits: a plan on the
+ * device memory (tight serving loops, harnesses that forbid hipMalloc, code that captures
+ * the plan's stream -- cfdj_fps_stream -- into a HIP graph).  The half spectrum lives in a
+ * static device array of the library instead of the plan's buffer; the call itself runs only
+ * the three hand-written FFT passes on the plan's stream (no hipMalloc / hipFree / rocFFT),
+ * no sync.  Limits: a plan on the
  * CFDJ_POISSON_FUSED path and (nx/2)*ny <= 1048576 complex elements (16 MiB, e.g.
  * 2048 x 1024 or 1024 x 1024); larger or rocFFT-path plans return CFDJ_ERR_ARG.  All calls
  * on one GPU share that GPU's array (any plan, any stream): calls that overlap on one GPU
  * race; nothing in it needs clearing between calls. */
 int cfdj_fps_solve_device_noalloc(cfdj_fps_plan* h, const double* f_dev, double* s_dev);
+/* The plan's HIP stream (a hipStream_t, created hipStreamNonBlocking) on which
+ * cfdj_fps_solve_device and cfdj_fps_solve_device_noalloc enqueue their kernels: for callers
+ * that order their own work against the solve (events, hipStreamSynchronize) or capture it. */
+int cfdj_fps_stream(cfdj_fps_plan* h, void** hip_stream);
 /* Select the Poisson implementation (CFDJ_POISSON_*); ARG error if unsupported. */
 int cfdj_fps_set_poisson(cfdj_fps_plan* h, int path);
 /* The implementation in use (CFDJ_POISSON_ROCFFT or CFDJ_POISSON_FUSED; ARG on NULL). */
@@ -202,7 +207,9 @@ int cfdj_cavity_upload(cfdj_cavity* h, const double* wn, long ldw, const double*
 int cfdj_cavity_download(cfdj_cavity* h, double* wn, long ldw, double* sn, long lds);
 /* nsteps RK3 steps; rms[k] (may be NULL) = lid_driven_cavity.jl:112-114 of step k. */
 int cfdj_cavity_step(cfdj_cavity* h, double dt, int nsteps, double* rms);
-/* lid_driven_cavity.jl:124-159 `rhs`: r interior from w, s (r boundary left 0). */
+/* lid_driven_cavity.jl:124-159 `rhs`: r interior from w, s (r boundary left 0).  A function
+ * of its arguments: the handle's vorticity and streamfunction are not touched (only stage
+ * scratch is), so it may be called between cfdj_cavity_upload and cfdj_cavity_step. */
 int cfdj_cavity_rhs(cfdj_cavity* h, const double* w, long ldw, const double* s, long lds,
                     double* r, long ldr);
 /* Total V-cycles run by the multigrid Poisson solves so far. */
@@ -264,8 +271,9 @@ int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu);
 /* w_f itself, complex nx x ny column-major as interleaved (re, im) doubles.  w_f is the
  * spectrum of a real field (the only kind the reference's loop produces): where the solver
  * keeps half of it (square power-of-two grids of 1024..8192, hybrid and 2/3 rule),
- * set_spectrum and jacobian read the modes kx index 0..nx/2 and take the others to be their
- * conjugate mirror, and get_spectrum returns exactly that mirror. */
+ * set_spectrum and jacobian keep the Hermitian part (w_f(k) + conj(w_f(-k))) / 2 of their
+ * input -- all that the reference's jacobian() sees through real(ifft(.)), so cfdj_spec_jacobian
+ * matches it for any input -- and get_spectrum returns that part with its conjugate mirror. */
 int cfdj_spec_get_spectrum(cfdj_spec* h, double* wf);
 int cfdj_spec_set_spectrum(cfdj_spec* h, const double* wf);
 /* One `jacobian(nx, ny, dx, dy, wf, k2)` call: jf = fft(-J(w, psi)) (complex, as above). */

@@ -52,6 +52,43 @@ def fps_sine(f, dx, dy, iden=None):
     return s
 
 
+def ps_fst(f, dx, dy):
+    """14_Poisson_Solver_FST/fft_d.jl:7-23: the same solve with the symbol DIVIDED into the
+    sine coefficients (fft_d.jl:15-20) instead of multiplied by a tabulated reciprocal;
+    f is (nx+1, ny+1), returns the (nx-1, ny-1) interior solution."""
+    nx, ny = f.shape[0] - 1, f.shape[1] - 1
+    e = sfft.dstn(np.array(f[1:nx, 1:ny]), type=1)
+    cx = np.array([math.cos(math.pi * k / nx) for k in range(1, nx)])
+    cy = np.array([math.cos(math.pi * k / ny) for k in range(1, ny)])
+    data1 = e / ((2.0 / dx ** 2) * (cx[:, None] - 1.0) + (2.0 / dy ** 2) * (cy[None, :] - 1.0))
+    return sfft.dstn(data1, type=1) / (2 * nx * 2 * ny)
+
+
+def fft_d_mms(nx, km=16):
+    """fft_d.jl:26-62: the manufactured solution of 12/fft_p.jl on the unit box (its
+    right-hand side is odd about every wall, so it is also a Dirichlet problem)."""
+    dx = dy = (1.0 - 0.0) / nx
+    x = 0.0 + dx * np.arange(nx + 1)
+    X, Y = x[:, None], x[None, :]
+    tp = 2 * math.pi
+    c1, c2 = (1.0 / km) ** 2, -8 * math.pi ** 2
+    ue = np.sin(tp * X) * np.sin(tp * Y) + c1 * np.sin(km * tp * X) * np.sin(km * tp * Y)
+    f = c2 * np.sin(tp * X) * np.sin(tp * Y) + c2 * np.sin(km * tp * X) * np.sin(km * tp * Y)
+    return f, ue, dx, dy
+
+
+def fft_d_mms_error(nx, solver="ps_fst"):
+    """fft_d.jl:64-75: (L2 over all (nx+1)(ny+1) nodes, Linf) of un - ue."""
+    f, ue, dx, dy = fft_d_mms(nx)
+    un = np.zeros_like(f)
+    if solver == "ps_fst":
+        un[1:nx, 1:nx] = ps_fst(f, dx, dy)
+    else:
+        un = fps_sine(f, dx, dy)
+    err = un - ue
+    return float(np.sqrt(np.sum(err ** 2) / ((nx + 1) * (nx + 1)))), float(np.abs(err).max())
+
+
 def bc2(w, s, dx, dy):
     """lid_driven_cavity.jl:39-51 (Jensen, 2nd order), in place; the i-loop (bottom/top)
     runs second and overwrites the corners."""

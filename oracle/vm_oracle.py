@@ -172,6 +172,16 @@ def compute_l2norm_bnds(r):
     return math.sqrt(float(np.sum(r * r)) / r.size)
 
 
+def fft_d_order_tolerance(nx, ref):
+    """Relative tolerance for comparing the L2 error of 14/fft_d.jl's DST-I solve with the
+    order.jl:11 value `ref` of 12/fft_p.jl on the same manufactured solution: 1e-9, or --
+    on the finer grids -- the rounding of the two scripts' symbols, which cancel from
+    O(nx^2) terms to 8 pi^2 for the dominant mode (relative error 4 nx^2 eps / (8 pi^2) of
+    the mode's unit amplitude, seen in an error norm of size ref)."""
+    sym = 4.0 * nx * nx * np.finfo(np.float64).eps / (8.0 * math.pi ** 2)
+    return max(1e-9, sym / ref)
+
+
 def fft_p_mms(nx, km=16):
     """fft_p.jl:45-82 MMS on [0,1]² (returns f, ue on the (nx+1)² node grid, and Δx)."""
     ny = nx

@@ -30,6 +30,21 @@ def smooth_field(nx, ny, kmax, seed):
     return w
 
 
+def smooth_field_fast(nx, ny, kmax, seed):
+    """The same field as smooth_field (same draws, same modes) assembled from products of
+    1-D cos / sin tables -- cos(kx x + ky y) = cos kx x cos ky y - sin kx x sin ky y -- as four
+    matrix products instead of (2 kmax + 1)^2 full-grid passes; equal to smooth_field up to
+    rounding.  For the large GPU test grids (not for the committed fixtures)."""
+    rng = np.random.default_rng(seed)
+    dx, dy, x, y = vo.vm_grid(nx, ny)
+    k = np.arange(-kmax, kmax + 1)
+    ab = rng.standard_normal((k.size, k.size, 2)) / (1.0 + k[:, None] ** 2 + k[None, :] ** 2)[..., None]
+    A, B = ab[..., 0], ab[..., 1]
+    cx, sx = np.cos(np.outer(x[:nx], k)), np.sin(np.outer(x[:nx], k))
+    cy, sy = np.cos(np.outer(k, y[:ny])), np.sin(np.outer(k, y[:ny]))
+    return cx @ (A @ cy + B @ sy) + sx @ (B @ cy - A @ sy)
+
+
 def main():
     out = {}
     # FD-FFT Poisson on the fft_p.jl MMS (12_Poisson_Solver_FFT/fft_p.jl:67-92)

@@ -239,3 +239,63 @@ def test_gpu_mg_fused_kernels_are_bit_identical(lib, monkeypatch, n, levels, swe
     assert np.array_equal(out["nodesc"][1], out["plain"][1])
     np.testing.assert_allclose(out["fused"][1], out["plain"][1], rtol=1e-13)
     np.testing.assert_allclose(out["narrow"][1], out["plain"][1], rtol=1e-13)
+
+
+@pytest.mark.parametrize("i", range(5))
+def test_gpu_fft_d_matches_order_jl(lib, i):
+    """14_Poisson_Solver_FST/fft_d.jl:47-75 on the GPU DST-I (cfd_julia_amd.fft_d over
+    cfdj_fps_sine) at N = 32 ... 512 against the reference-held L2 errors of order.jl:11.
+    Those are the errors of 12/fft_p.jl; they pin fft_d.jl as well because the manufactured
+    right-hand side is odd about every wall of the unit box: the zero-mean periodic 5-point
+    solution is then odd, vanishes on the walls and solves fft_d.jl's Dirichlet system too
+    -- one discrete field, one norm (compute_l2norm_bnds).  Tolerance 1e-9 relative up to
+    N = 128; at 256 and 512 the rounding of the two scripts' own symbols (cancellation from
+    O(nx^2) to 8 pi^2) bounds the agreement at 1e-8 / 1.6e-7 (vo.fft_d_order_tolerance; the
+    CPU oracle differs from order.jl:11 by 1.8e-9 / 2.9e-8 there)."""
+    from cfd_julia_amd import fft_d
+    from oracle import vm_oracle as vo
+
+    n = vo.ORDER_JL_GRID[i]
+    l2, linf = fft_d.main(grids=(n,))[n]
+    ref = vo.ORDER_JL_FFT_FDM[i]
+    assert abs(l2 - ref) / ref < vo.fft_d_order_tolerance(n, ref), (n, l2, ref)
+    assert linf < 4 * ref  # two modes: the maximum norm stays within a few L2 norms
+
+
+def test_gpu_fft_d_default_run_matches_oracle(lib):
+    """fft_d.jl's shipped run (nx = ny = 128): the interior solution against the oracle's
+    restatement (division by the symbol, fft_d.jl:15-20), 1e-12 of max|u|."""
+    from cfd_julia_amd import fft_d
+
+    f, ue, dx, dy = fft_d.mms(128)
+    u = fft_d.ps_fst(128, 128, dx, dy, f)
+    ref = co.ps_fst(f, dx, dy)
+    assert u.shape == (127, 127)
+    assert np.abs(u - ref).max() < 1e-12 * np.abs(ref).max()
+
+
+def test_gpu_cavity_rhs_call_leaves_the_state_alone(lib):
+    """cfdj_cavity_rhs (lid_driven_cavity.jl:124-159 as a function of the caller's w, s) between
+    an upload and a step: the step continues from the uploaded fields -- the psi the caller
+    hands to rhs, here with non-zero wall values, must not leak into either of the handle's
+    two psi buffers."""
+    from cfd_julia_amd.cavity import Cavity
+
+    n, nt = 64, 2
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    dt = 1e-3
+    rng = np.random.default_rng(18)
+    w0 = np.asfortranarray(np.pad(smooth_field(n - 1, n - 1, 3, 71), ((1, 1), (1, 1))))
+    s0 = np.asfortranarray(np.pad(1e-2 * smooth_field(n - 1, n - 1, 3, 72), ((1, 1), (1, 1))))
+    wx = np.asfortranarray(rng.standard_normal((n + 1, n + 1)))
+    sx = np.asfortranarray(rng.standard_normal((n + 1, n + 1)))  # walls != 0
+    with Cavity(n, n, dx, dy, 100.0) as h:
+        h.upload(w0, s0)
+        r = h.rhs(wx, sx)
+        rms = h.step(dt, nt)
+        wn, sn = h.download()
+    assert np.array_equal(r, co.cavity_rhs(wx, sx, dx, dy, 100.0))
+    w_ref, s_ref, rms_ref = co.cavity_numerical(n, n, nt, dt, 100.0, wn=w0, sn=s0)
+    assert np.abs(wn - w_ref).max() < 1e-10 * max(1.0, np.abs(w_ref).max())
+    assert np.abs(sn - s_ref).max() < 1e-12
+    assert np.allclose(rms, rms_ref, rtol=1e-8, atol=1e-16)

@@ -113,3 +113,34 @@ def test_gpu_schur_path_selection(cfdj):
         assert h.poisson() == "fused"
         h.set_poisson("auto")
         assert h.poisson() == "schur"
+
+
+@pytest.mark.parametrize("n,P,path", [(2048, 4, "schur"), (4096, 8, "schur"), (4096, 2, "schur"),
+                                      (1024, 2, "fused"), (256, 2, "rocfft")])
+def test_gpu_virtual_slabs_side_stream_schedule_is_bit_identical(cfdj, monkeypatch, n, P, path):
+    """The multi-GPU step's event schedule on one GPU: virtual slabs created with
+    CFDJ_VIRTUAL_OVERLAP=1 run what the RCCL ranks run -- halo exchanges on the side stream
+    (omega during the Poisson passes, psi during the interior rows of the stage kernel) and the
+    substructured solve's two gathers on the side stream behind their four events -- with
+    device copies in place of the collectives.  What a slab contributes to a gather goes to a
+    staging buffer and reaches the shared arrays only through the side stream's copy, so a
+    consumer that did not wait for its event would read the previous solve's values.  Several
+    steps over several calls must equal the single-stream order bit for bit, and the oracle
+    to the north-star tolerance."""
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    dt = min(0.01, 5e-4 * (4096 / n) ** 2)
+    out = {}
+    for ov in ("0", "1"):
+        monkeypatch.setenv("CFDJ_VIRTUAL_OVERLAP", ov)
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+            h.set_poisson(path)
+            assert h.poisson() == path
+            h.upload_interior(w0)
+            h.step(dt, 2)
+            h.step(dt, 1)
+            out[ov] = h.download_interior()
+    assert np.array_equal(out["0"], out["1"])
+    if n <= 2048:
+        ref = vo.numerical(w0, 3, dt, dx, dy, 1000.0)
+        assert np.abs(out["1"] - ref).max() < 1e-10

@@ -15,7 +15,7 @@ import numpy as np
 import pytest
 
 from oracle import vm_oracle as vo
-from tests.golden.make_golden import smooth_field
+from tests.golden.make_golden import smooth_field, smooth_field_fast
 
 pytestmark = pytest.mark.gpu
 
@@ -31,7 +31,8 @@ def cfdj():
 
 def field(nx, ny, seed):
     rng = np.random.default_rng(seed)
-    return np.asfortranarray(smooth_field(nx, ny, 3, seed) + 0.01 * rng.standard_normal((nx, ny)))
+    smooth = smooth_field_fast if nx * ny >= 1 << 22 else smooth_field
+    return np.asfortranarray(smooth(nx, ny, 3, seed) + 0.01 * rng.standard_normal((nx, ny)))
 
 
 @pytest.mark.parametrize("nx,ny", [(2048, 1024), (4096, 2048), (8192, 1024), (16384, 1024),

@@ -196,8 +196,10 @@ def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
 
 @pytest.mark.parametrize("kind", ["hybrid", "2/3"])
 def test_gpu_spectral_half_spectrum_round_trip(spec, kind):
-    """set_spectrum / spectrum through the half-spectrum state (n = 1024): the full spectrum
-    of a real field comes back bit for bit, its Nyquist row and column included."""
+    """set_spectrum / spectrum through the half-spectrum state (n = 1024): the Hermitian part
+    (w_f(k) + conj(w_f(-k))) / 2 of what went in comes back bit for bit, its Nyquist row and
+    column included -- for the spectrum of a real field that is the spectrum itself, up to
+    the last-bit asymmetries of the CPU FFT that produced it."""
     n = 1024
     dx, dy, _, _ = vo.vm_grid(n, n)
     f = smooth_field(n, n, 5, n) + 0.01 * np.random.default_rng(7).standard_normal((n, n))
@@ -205,10 +207,13 @@ def test_gpu_spectral_half_spectrum_round_trip(spec, kind):
     with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
         h.set_spectrum(wf)
         back = h.spectrum()
-    i = np.arange(n // 2 + 1)
-    assert np.array_equal(back[i, :], wf[i, :])
     mirror = np.conj(wf[(-np.arange(n)) % n][:, (-np.arange(n)) % n])
-    assert np.array_equal(back[n // 2 + 1:, :], mirror[n // 2 + 1:, :])
+    herm = 0.5 * (wf + mirror)
+    assert np.abs(herm - wf).max() <= 1e-15 * np.abs(wf).max()
+    i = np.arange(n // 2 + 1)
+    assert np.array_equal(back[i, :], herm[i, :])
+    hm = np.conj(herm[(-np.arange(n)) % n][:, (-np.arange(n)) % n])
+    assert np.array_equal(back[n // 2 + 1:, :], hm[n // 2 + 1:, :])
 
 
 @pytest.mark.parametrize("kind", KINDS)
@@ -244,3 +249,21 @@ def test_gpu_spectral_argument_errors(spec):
         spec.SpectralNS2D(64, 32, dx, dx, 1000.0)  # ky = kx aliasing: square only
     with pytest.raises(_lib.ArgumentError):
         spec.SpectralNS2D(63, 63, dx, dx, 1000.0)  # odd nx
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_gpu_spectral_jacobian_of_a_non_hermitian_spectrum(spec, kind):
+    """hybrid.jl:92-152 / pseudospectral_23_rule.jl:95-144 take real(ifft(.)) of what they are
+    given, i.e. they see the Hermitian part of w_f only (the 3/2 rule's padded Nyquist modes
+    apart, pseudospectral_32_rule.jl:124-133).  A w_f that is NOT the spectrum of a real field
+    must therefore give the oracle's Jacobian on the half-spectrum path (n = 1024) as on the
+    full-spectrum ones (n = 96: library transforms, n = 256: hand-written)."""
+    for n in (96, 256, 1024):
+        dx, dy, _, _ = vo.vm_grid(n, n)
+        rng = np.random.default_rng(7 * n)
+        wf = _noisy_spectrum(n) + n * (rng.standard_normal((n, n))
+                                       + 1j * rng.standard_normal((n, n)))
+        ref = so.JACOBIANS[KIND_ID[kind]](wf, so.wavespace(n, n, dx, dy), dx, dy)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+            got = h.jacobian(wf)
+        assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), n

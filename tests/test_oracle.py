@@ -38,6 +38,31 @@ def test_fft_s_spectral_is_roundoff(i):
     assert 0.5 * ref < l2 < 2.0 * ref, (n, l2, ref)
 
 
+@pytest.mark.parametrize("solver", ["ps_fst", "fps_sine"])
+@pytest.mark.parametrize("i", range(5))
+def test_fft_d_matches_order_jl(i, solver):
+    """14_Poisson_Solver_FST/fft_d.jl:47-75 runs the manufactured solution of 12/fft_p.jl
+    (order.jl:11 holds that script's L2 errors) through the DST-I solver.  The right-hand
+    side is odd about every wall of the unit box, so the zero-mean periodic 5-point solution
+    of fft_p.jl is odd too, vanishes on the walls, and therefore IS the solution of the
+    Dirichlet 5-point system fft_d.jl solves: same discrete field, same norm
+    (compute_l2norm_bnds over all (nx+1)(ny+1) nodes), hence order.jl:11's numbers pin the
+    sine-transform solver (the cavity's fps_sine, lid_driven_cavity.jl:11-21, is the same
+    solve with the reciprocal symbol tabulated).
+    Tolerance: 1e-9 relative up to N = 128.  Beyond, the two scripts' own symbols limit the
+    agreement: (2/dx^2)(cos(pi i/nx) - 1) here and aa + bb cos kx + cc cos ky there both
+    cancel from O(nx^2) terms to 8 pi^2 for the dominant mode, each with its own rounding,
+    so the mode's amplitude carries a relative error of about 4 nx^2 eps / (8 pi^2) and the
+    (much smaller) L2 error norm that amount divided by itself: 1e-8 at 256, 1.6e-7 at 512
+    (measured differences: 1.8e-9 and 2.9e-8)."""
+    from oracle import cavity_oracle as co
+
+    n = vo.ORDER_JL_GRID[i]
+    l2, _ = co.fft_d_mms_error(n, solver)
+    ref = vo.ORDER_JL_FFT_FDM[i]
+    assert abs(l2 - ref) / ref < vo.fft_d_order_tolerance(n, ref), (n, solver, l2, ref)
+
+
 def test_kx_table_reference_layout():
     kx = vo.kx_table(8, 1e-6)
     hx = 2 * math.pi / 8
