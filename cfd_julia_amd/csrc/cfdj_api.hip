@@ -146,27 +146,19 @@ struct cfdj_vm {
   // substructured y-slab solve (schur.hip): traces of all ranks T, gathered column G
   SchurTables schur;
   bool use_schur = false;
-  double2* T = nullptr;
+  // gather buffer of the substructured solve: per rank [4 L trace numbers][rows elements of
+  // the packed column]; G: the solved packed column, dense
+  double2* TG = nullptr;
   int ncp = 0;  // column-sum partial rows (blocks of rows_per_wave rows)
   double2* G = nullptr;
-  // virtual slabs with the side-stream schedule: what a rank contributes to an all-gather
-  // goes to these staging copies first and reaches G / T only through the side stream's
-  // copy (the stand-in for the collective), so a consumer that does not wait for it reads
-  // the previous solve's values, as it would on real ranks
-  double2 *Gs = nullptr, *Ts = nullptr;
+  size_t tg_block() const { return (size_t)4 * (nx / 2) + (size_t)rows; }
   rocfft_plan g_fwd = nullptr, g_inv = nullptr;
   ncclComm_t comm = nullptr;
-  // RCCL slabs: halo exchanges on a side stream, overlapped with the Poisson passes (omega
+  // y-slabs: halo exchanges on a side stream, overlapped with the Poisson passes (omega
   // halo) and the interior rows of the stage kernel (psi halo).  Collectives stay strictly
   // ordered: the main stream waits for the omega halo before its first collective.
   hipStream_t side = nullptr;
   hipEvent_t ev_src = nullptr, ev_whalo = nullptr, ev_psi = nullptr, ev_shalo = nullptr;
-  // ... and the substructured solve's two all-gathers: the packed column's during the trace
-  // pass, the traces' during the packed column's own solve (gather_on_side, set by the
-  // overlapped stage); every RCCL operation of a step is then on the side stream, in program
-  // order, the same on every rank
-  hipEvent_t ev_g = nullptr, ev_g2 = nullptr, ev_t = nullptr, ev_t2 = nullptr;
-  bool gather_on_side = false;
   bool whalo_pending = false;
   double* gather = nullptr;                                      // Rccl download buffer
   // timing
@@ -399,20 +391,22 @@ struct cfdj_vm {
     }
   }
 
-  // y-slabs without a transpose (schur.hip): row r2c -> interior traces -> all-gather of
-  // 4 numbers per x-mode -> separator solve + interior solve -> row c2r.  The packed
-  // DC / Nyquist column is gathered and solved with the reference symbol: by the single-GPU
-  // column kernel for columns of up to 8192, by library transforms beyond.
+  // y-slabs without a transpose (schur.hip): row r2c -> interior traces -> ONE all-gather of
+  // every rank's traces (4 numbers per x-mode) and its piece of the packed DC / Nyquist column
+  // -> that column's solve (one workgroup) -> separator + interior solve -> row c2r.
+  // The gather buffer TG holds one block per rank, [4 L trace numbers][rows column elements];
+  // a rank's own block is where its kernels write (in-place all-gather).  The packed column
+  // is solved with the reference symbol: columns of up to 8192 by col0_solve_kernel straight
+  // from the blocks, longer ones by library transforms on the dense copy G.
   void poisson_schur(const std::vector<const double*>& src, bool neg) {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
     const bool col0_direct = fused_rows_take_col0(nx, rows);
-    // the exchanges on the side stream (RCCL ranks, or virtual slabs rehearsing that schedule
-    // with staged device copies)
-    const bool aside = gather_on_side && side != nullptr;
-    const bool staged = aside && mode == Mode::Virtual;
-    auto schur_args = [&](const Slab& s, bool trace_pass) {
-      SchurArgs sa = schur.args(s.X, staged && trace_pass ? Ts : T, s.rank, out_scale, ny);
+    const size_t blk = tg_block();
+    auto col_piece = [&](const Slab& s) { return TG + (size_t)s.rank * blk + (size_t)4 * L; };
+    auto schur_args = [&](const Slab& s) {
+      SchurArgs sa = schur.args(s.X, TG, s.rank, out_scale, ny);
+      sa.tstride = blk;
       sa.tile8 = 1;
       sa.cs = s.cs;
       return sa;
@@ -440,74 +434,48 @@ struct cfdj_vm {
       a.push_back(fused.args(sym, src[i], slabs[i].psi, slabs[i].X, slabs[i].X, rows,
                              slabs[i].rank, nranks, neg));
       a.back().tile8 = 1;  // 8-mode tiles: whole-line row writes, shared column reads
-      // column m = 0 (packed DC / Nyquist) straight to and from the gathered column G
       if (col0_direct) {
+        // column m = 0 (packed DC / Nyquist): written straight into the rank's block of the
+        // gather buffer by pass 0, read from the solved dense column G by pass 2
         a.back().col0 = G + slabs[i].row0;
         a.back().fx = slabs[i].cs8;
         a.back().Hx = slabs[i].cs;
       }
     }
-    double2* Gw = staged ? Gs : G;  // where the ranks put their pieces of the packed column
     for (size_t i = 0; i < a.size(); ++i) {
       FusedPoissonArgs a0 = a[i];
-      if (col0_direct) a0.col0 = Gw + slabs[i].row0;
+      if (col0_direct) a0.col0 = col_piece(slabs[i]);
       tbegin(CFDJ_K_FFT_FWD);
       launch_fused_poisson_pass(0, a0, stream);
       tend();
     }
-    // column m = 0 (packed DC / Nyquist) of the tiled spectrum: element j at 8 j
-    tbegin(CFDJ_K_COMM);
-    if (!col0_direct)
-      for (auto& s : slabs) launch_strided_copy(Gw + s.row0, 1, s.X, 8, rows, stream);
-    if (aside) {
-      CFDJ_HIP(hipEventRecord(ev_g, stream));
-      CFDJ_HIP(hipStreamWaitEvent(side, ev_g, 0));
-      if (mode == Mode::Rccl)
-        CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, side));
-      else
-        CFDJ_HIP(hipMemcpyAsync(G, Gs, (size_t)ny * sizeof(double2), hipMemcpyDeviceToDevice,
-                                side));
-      CFDJ_HIP(hipEventRecord(ev_g2, side));
-    } else if (mode == Mode::Rccl) {
-      comm_order();
-      CFDJ_NCCL(ncclAllGather(G + slabs[0].row0, G, 2 * (size_t)rows, ncclDouble, comm, stream));
+    if (!col0_direct) {  // column 0 of the tiled spectrum: element j at 8 j
+      tbegin(CFDJ_K_COMM);
+      for (auto& s : slabs) launch_strided_copy(col_piece(s), 1, s.X, 8, rows, stream);
+      tend();
     }
-    tend();
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
-      launch_schur_pass(0, schur_args(s, true), stream);
+      launch_schur_pass(0, schur_args(s), stream);
       tend();
     }
-    if (mode == Mode::Rccl || staged) {
+    if (mode == Mode::Rccl) {
+      // on the main stream: both solves below wait for it anyway, and a hop to another stream
+      // and back costs more than the exchange hides
       tbegin(CFDJ_K_COMM);
-      const size_t cnt = (size_t)L * 4 * 2;  // doubles per rank
-      hipStream_t cs = stream;
-      if (aside) {
-        CFDJ_HIP(hipEventRecord(ev_t, stream));
-        CFDJ_HIP(hipStreamWaitEvent(side, ev_t, 0));
-        cs = side;
-      }
-      if (mode == Mode::Rccl)
-        CFDJ_NCCL(ncclAllGather(reinterpret_cast<double*>(T) + (size_t)rank * cnt, T, cnt,
-                                ncclDouble, comm, cs));
-      else
-        CFDJ_HIP(hipMemcpyAsync(T, Ts, (size_t)nranks * cnt * sizeof(double),
-                                hipMemcpyDeviceToDevice, cs));
-      if (aside) CFDJ_HIP(hipEventRecord(ev_t2, side));
+      comm_order();
+      CFDJ_NCCL(ncclAllGather(reinterpret_cast<double*>(TG + (size_t)rank * blk), TG, 2 * blk,
+                              ncclDouble, comm, stream));
       tend();
     }
-    // the packed column's solve needs the gathered column only; the interior solve the
-    // gathered traces only
-    if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_g2, 0));
     tbegin(CFDJ_K_DIVIDE);
-    if (fused_poisson_supported(nx, ny, ny)) {
-      // the gathered column is column 0 of a one-column spectrum: the single-GPU column
-      // pass (forward FFT, packed divide, inverse FFT in one workgroup)
-      FusedPoissonArgs ga = fused.args(sym, nullptr, nullptr, G, G, ny, 0, 1, neg);
-      ga.kb = 1;
-      ga.seg = (unsigned)ny;
-      launch_fused_poisson_pass(1, ga, stream);
+    FusedPoissonArgs ga = fused.args(sym, nullptr, nullptr, G, G, ny, 0, 1, neg);
+    if (col0_solve_supported(ny)) {
+      launch_col0_solve(ga, TG + (size_t)4 * L, blk, rows, G, stream);
     } else {
+      for (int q = 0; q < nranks; ++q)
+        launch_strided_copy(G + (size_t)q * rows, 1, TG + (size_t)q * blk + (size_t)4 * L, 1, rows,
+                            stream);
       plans.exec(g_fwd, G, nullptr);
       PackedDivParams pd;
       pd.Z = G;
@@ -524,16 +492,16 @@ struct cfdj_vm {
       plans.exec(g_inv, G, nullptr);
     }
     tend();
-    if (aside) CFDJ_HIP(hipStreamWaitEvent(stream, ev_t2, 0));
     for (auto& s : slabs) {
       tbegin(CFDJ_K_DIVIDE);
-      launch_schur_pass(1, schur_args(s, false), stream);
+      launch_schur_pass(1, schur_args(s), stream);
       tend();
     }
-    tbegin(CFDJ_K_COMM);
-    if (!col0_direct)
+    if (!col0_direct) {
+      tbegin(CFDJ_K_COMM);
       for (auto& s : slabs) launch_strided_copy(s.X, 8, G + s.row0, 1, rows, stream);
-    tend();
+      tend();
+    }
     for (auto& ai : a) {
       tbegin(CFDJ_K_FFT_INV);
       launch_fused_poisson_pass(2, ai, stream);
@@ -623,23 +591,17 @@ struct cfdj_vm {
     halo(false, src, side);
     CFDJ_HIP(hipEventRecord(ev_whalo, side));
     whalo_pending = true;
-    gather_on_side = use_schur;
-    try {
-      poisson(src, true);
-    } catch (...) {
-      gather_on_side = false;
-      throw;
-    }
-    gather_on_side = false;
-    comm_order();  // paths without a collective on the main stream before the psi halo
+    poisson(src, true);
+    comm_order();  // (a no-op where the Poisson path had a collective on the main stream)
     CFDJ_HIP(hipEventRecord(ev_psi, stream));
     CFDJ_HIP(hipStreamWaitEvent(side, ev_psi, 0));
     std::vector<const double*> ps(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i) ps[i] = slabs[i].psi;
     halo(true, ps, side);
     CFDJ_HIP(hipEventRecord(ev_shalo, side));
-    // interior blocks first, then the first / last rows_per_wave rows (which read the halo
-    // rows); block-aligned, so the column partials match the one-launch order
+    // interior blocks first, then -- in one launch -- the first and the last rows_per_wave
+    // rows (which read the halo rows); block-aligned, so the column partials match the
+    // one-launch order
     const int rb = rows_per_wave;
     std::vector<StageParams> sp;
     for (size_t i = 0; i < slabs.size(); ++i) {
@@ -658,10 +620,10 @@ struct cfdj_vm {
     }
     CFDJ_HIP(hipStreamWaitEvent(stream, ev_shalo, 0));
     for (StageParams& p : sp) {
-      p.ycount = rb;
       p.y0 = 0;
-      launch_stage(st, p, stream);
-      p.y0 = rows - rb;
+      p.ycount = rb;
+      p.y0b = rows - rb;
+      p.ycount_b = rb;
       launch_stage(st, p, stream);
     }
   }
@@ -767,7 +729,7 @@ struct cfdj_vm {
   // side stream (default priority) and the events that order it against the main stream
   void create_side() {
     CFDJ_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    for (hipEvent_t* e : {&ev_src, &ev_whalo, &ev_psi, &ev_shalo, &ev_g, &ev_g2, &ev_t, &ev_t2})
+    for (hipEvent_t* e : {&ev_src, &ev_whalo, &ev_psi, &ev_shalo})
       CFDJ_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   }
 
@@ -810,7 +772,7 @@ struct cfdj_vm {
       rocfft_plan_description_destroy(desc);
       if (schur_ok(nx, ny, nranks)) {
         schur.init(nx, ny, dx, dy, eps, nranks);
-        T = dalloc<double2>((size_t)nranks * (nx / 2) * 4);
+        TG = dalloc<double2>((size_t)nranks * ((size_t)4 * (nx / 2) + (size_t)(ny / nranks)));
         G = dalloc<double2>((size_t)ny);
         g_fwd = plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 1,
                           &len_y, 1, nullptr);
@@ -850,16 +812,14 @@ struct cfdj_vm {
     sym.destroy();
     fused.destroy();
     schur.destroy();
-    dfree(T);
+    dfree(TG);
     dfree(G);
-    dfree(Gs);
-    dfree(Ts);
     dfree(spec);
     dfree(gather);
     dfree(d_flag);
     for (auto e : ev) (void)hipEventDestroy(e);
     if (side) (void)hipStreamSynchronize(side);
-    for (hipEvent_t e : {ev_src, ev_whalo, ev_psi, ev_shalo, ev_g, ev_g2, ev_t, ev_t2})
+    for (hipEvent_t e : {ev_src, ev_whalo, ev_psi, ev_shalo})
       if (e) (void)hipEventDestroy(e);
     if (side) (void)hipStreamDestroy(side);
     if (comm) ncclCommDestroy(comm);
@@ -873,7 +833,7 @@ struct cfdj_vm {
 namespace {
 
 cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int device,
-                Mode mode, int nranks, int rank) {
+                Mode mode, int nranks, int rank, int solo_rank = -1) {
   check_grid(nx, ny, dx, dy);
   CFDJ_REQUIRE(std::isfinite(re) && re != 0.0, "re must be finite and non-zero");
   CFDJ_REQUIRE(nranks >= 1 && ny % nranks == 0, "ny must be divisible by the rank count");
@@ -895,7 +855,12 @@ cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int
   // rows per wavefront: keep >= ~8 waves per CU at the benchmark sizes
   h->rows_per_wave = ny / nranks >= 2048 ? 32 : 8;  // measured sweep: 32 best at 4096^2
   CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
-  if (mode == Mode::Virtual) {
+  if (mode == Mode::Virtual && solo_rank >= 0) {
+    // one rank's share of the nranks-rank step, alone on this GPU: its slab only, every
+    // exchange a copy from itself (timing rehearsal: the field is not the global solution)
+    h->slabs.resize(1);
+    h->slabs[0].rank = solo_rank;
+  } else if (mode == Mode::Virtual) {
     h->slabs.resize(nranks);
     for (int p = 0; p < nranks; ++p) h->slabs[p].rank = p;
   } else {
@@ -1072,17 +1037,31 @@ int cfdj_vm_create_virtual(int nx, int ny, double dx, double dy, double re, doub
   return guard([&] {
     CFDJ_REQUIRE(out != nullptr, "out is NULL");
     *out = nullptr;
-    std::unique_ptr<cfdj_vm> h(new_vm(nx, ny, dx, dy, re, eps, device, Mode::Virtual, nranks, 0));
-    // CFDJ_VIRTUAL_OVERLAP=1: the RCCL ranks' side-stream schedule (halo exchanges and the
-    // substructured solve's two gathers behind events) with staged device copies standing in
-    // for the collectives -- the event graph of the multi-GPU step on one GPU
+    // CFDJ_VIRTUAL_SOLO_RANK=r: only rank r's slab (a timing rehearsal of one rank's compute)
+    int solo = -1;
+    if (const char* sr = std::getenv("CFDJ_VIRTUAL_SOLO_RANK")) {
+      solo = std::atoi(sr);
+      CFDJ_REQUIRE(solo >= 0 && solo < nranks, "CFDJ_VIRTUAL_SOLO_RANK out of range");
+    }
+    std::unique_ptr<cfdj_vm> h(
+        new_vm(nx, ny, dx, dy, re, eps, device, Mode::Virtual, nranks, 0, solo));
+    // CFDJ_VIRTUAL_OVERLAP=1: the RCCL ranks' side-stream schedule (halo exchanges behind
+    // events, interior / edge split of the stage kernel) with device copies standing in for
+    // the exchanges -- the event graph of the multi-GPU step on one GPU
     const char* ov = std::getenv("CFDJ_VIRTUAL_OVERLAP");
-    if (ov && ov[0] == '1') {
-      h->create_side();
-      if (h->T) {
-        h->Ts = dalloc<double2>((size_t)nranks * (nx / 2) * 4);
-        h->Gs = dalloc<double2>((size_t)ny);
-      }
+    if (ov && ov[0] == '1') h->create_side();
+    if (solo >= 0) {
+      // what the absent ranks would have delivered: zeros (finite, so the step stays sane)
+      const size_t L = (size_t)nx / 2;
+      auto zero = [](void* p, size_t bytes) {
+        if (p) CFDJ_HIP(hipMemset(p, 0, bytes));
+      };
+      zero(h->TG, (size_t)nranks * (4 * L + (size_t)h->rows) * sizeof(double2));
+      zero(h->G, (size_t)ny * sizeof(double2));
+      Slab& sl = h->slabs[0];
+      zero(sl.X, (size_t)h->nxh * h->rows * sizeof(double2));
+      zero(sl.S, (size_t)nranks * h->kb * h->rows * sizeof(double2));
+      zero(sl.Y, (size_t)ny * h->kb * sizeof(double2));
     }
     *out = h.release();
   });
@@ -1303,8 +1282,10 @@ int cfdj_vm_field_device(cfdj_vm* h, double** w_dev) {
 int cfdj_vm_slab(cfdj_vm* h, int* row0, int* rows) {
   return guard([&] {
     CFDJ_REQUIRE(h != nullptr, "NULL handle");
-    if (row0) *row0 = h->mode == Mode::Virtual ? 0 : h->slabs[0].row0;
-    if (rows) *rows = h->mode == Mode::Virtual ? h->ny : h->rows;
+    // virtual handles hold every slab (the whole grid), except the one-rank rehearsal
+    const bool all = h->mode == Mode::Virtual && (int)h->slabs.size() == h->nranks;
+    if (row0) *row0 = all ? 0 : h->slabs[0].row0;
+    if (rows) *rows = all ? h->ny : h->rows;
   });
 }
 

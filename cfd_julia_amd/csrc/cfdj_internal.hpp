@@ -139,7 +139,9 @@ struct StageParams {
   const double* wn;    // omega^n (pointwise; stages 2 and 3)
   double* out;         // stage output (stage 0: the bare RHS r)
   int nx, ny;
-  int y0, ycount;      // rows [y0, y0 + ycount) of the slab are computed (halo split)
+  int y0, ycount;      // rows [y0, y0 + ycount) of the slab are computed (halo split) ...
+  int y0b = 0, ycount_b = 0;  // ... and, in the same launch, rows [y0b, y0b + ycount_b)
+                       // (marching kernel only; both windows whole rows_per_wave blocks)
   double* colpart;     // optional: per-wave column sums of `out`, [y / rows_per_wave][nx]
   int rows_per_wave;
   bool march;          // true: always the marching kernel (rows_per_wave rows per wavefront)
@@ -302,7 +304,9 @@ void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, doubl
 // 2 rl in LDS), separators by a P x P circulant system from the gathered traces.
 struct SchurArgs {
   double2* H;           // this rank's half spectrum in 8-mode tiles, rl rows (in place)
-  double2* T;           // [P][L][4] traces of every rank: f_sep, t_1, t_n, column sum
+  double2* T;           // traces of every rank: rank q's [L][4] block (f_sep, t_1, t_n,
+                        // column sum) starts at T + q * tstride
+  size_t tstride;       // complex elements between two ranks' blocks (>= 4 L)
   const double* cinv;   // [L][P] first row of the inverse circulant separator system
   const double* corr;   // [L] 1/D_ref(m, 0) - 1/e_m (the reference's ky[1] = eps)
   const double* g;      // trace Green's function gL(j), j = 0..rl, in 8-mode tiles
@@ -333,6 +337,16 @@ struct PackedDivParams {
   bool neg;
 };
 void launch_packed_divide(const PackedDivParams& p, hipStream_t st);
+
+// The packed DC / Nyquist column of the y-slab path solved whole by ONE workgroup, everything
+// in LDS: the column's ny elements are read from P rank segments of `rows` elements (segment
+// q at src + q * seg_stride: the all-gather's receive layout), transformed along y, split into
+// the DC and the Nyquist column with the Z[k], Z[-k] symmetry, each divided by its reference
+// symbol (e[1,1] = 0), re-packed, transformed back and written to the dense column `dst`.
+// ny = 1024..8192 (a power of two); `a` supplies the symbol tables, the twiddles and `neg`.
+bool col0_solve_supported(int ny);
+void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg_stride,
+                       int rows, double2* dst, hipStream_t st);
 
 // Finiteness check: sets *flag = 1 if any element is not finite.
 void launch_check_finite(const double* a, size_t n, int* flag, hipStream_t st);

@@ -420,6 +420,7 @@ struct SchurTables {
     SchurArgs a;
     a.H = H;
     a.T = T;
+    a.tstride = (size_t)4 * L;
     a.cinv = cinv;
     a.corr = corr;
     a.g = g;

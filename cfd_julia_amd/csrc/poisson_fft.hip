@@ -388,6 +388,54 @@ __global__ __launch_bounds__((Plan<M, kColsNV>::T))
   cols_column<M, MIRROR, false, kColsNV, kColsHalf>(lds, col, ocol, m, tid, twM, da);
 }
 
+// The packed column alone, for the y-slab path (every rank solves the gathered column
+// redundantly, on its step's critical path): one workgroup, the whole column in a complex LDS
+// buffer, the partner Z[-k] of the packed divide read back from that buffer -- no round trip
+// through global memory as in cols_column's packed branch (which must not cost the other 2047
+// columns' workgroups any registers).  Element y of the column comes from segment y >> rl_log2
+// of `src` (the all-gather's receive layout), the result goes to the dense column `dst`.
+template <int M>
+__global__ __launch_bounds__((Plan<M>::T)) void col0_solve_kernel(
+    const double2* __restrict__ src, size_t seg_stride, int rl_log2, double2* __restrict__ dst,
+    const double2* __restrict__ twM_, const DivArgs da) {
+  using P = Plan<M>;
+  __shared__ double2 lds[P::PAD];
+  const TwGlobal<M> twM{twM_};
+  const int tid = threadIdx.x;
+  const double sgn = da.neg ? -1.0 : 1.0;
+  double2 a[16];
+  constexpr int R0 = P::radix(0);
+#pragma unroll
+  for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+    for (int r = 0; r < R0; ++r) {
+      const int y = in_pos<M, 0>(tid, b, r);
+      a[b * R0 + r] = src[(size_t)(y >> rl_log2) * seg_stride + (y & ((1 << rl_log2) - 1))];
+    }
+  col_fft<M, -1, false>(lds, a, tid, twM);
+  double2 v[16];
+  fwd_to_inv<M>(a, v);  // v[r] = Z[k], k = tid + T r
+  __syncthreads();       // the forward transform's last LDS reads
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lds[padx(tid + P::T * r)] = v[r];
+  __syncthreads();
+  const double ax = fd_symbol_x(da.aa, da.bb, da.cx[0]);
+  const double axL = fd_symbol_x(da.aa, da.bb, da.cx[da.L]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int k = tid + P::T * r;
+    const double2 Zp = lds[padx((M - k) & (M - 1))];
+    v[r] = packed_divide(v[r], Zp, k, ax, axL, da, sgn, false);
+  }
+  col_fft<M, 1, false>(lds, v, tid, twM);  // (its first LDS write is behind a barrier)
+  constexpr int SL = P::NSTAGES - 1;
+  constexpr int RL = P::radix(SL);
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) dst[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
+}
+
 // ---------------------------------------------------------------------------------------
 // Pass 3: rows, packed half spectrum -> real (c2r).
 // ---------------------------------------------------------------------------------------
@@ -830,6 +878,25 @@ bool fused_rows_take_col0(int nx, int rows) {
 bool fused_poisson_supported(int nx, int ny, int rows) {
   return pow2(nx) && pow2(ny) && nx >= 1024 && nx <= 16384 && ny >= 1024 && ny <= 8192 &&
          rows >= 8 && rows % 8 == 0 && ny % rows == 0;
+}
+
+bool col0_solve_supported(int ny) { return pow2(ny) && ny >= 1024 && ny <= 8192; }
+
+void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg_stride,
+                       int rows, double2* dst, hipStream_t st) {
+  if (!col0_solve_supported(a.ny) || rows < 1 || !pow2(rows) || a.ny % rows != 0 ||
+      a.cy_mirror != nullptr)
+    throw Error{CFDJ_ERR_ARG, "packed column solve: unsupported size"};
+  const DivArgs da{a.cx,  a.cy,  nullptr,           a.aa, a.bb, a.cc,       a.scale,
+                   a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, 0, ilog2(rows), 0u};
+  const int rl_log2 = ilog2(rows);
+  switch (a.ny) {
+    case 1024: hipLaunchKernelGGL((col0_solve_kernel<1024>), dim3(1), dim3(Plan<1024>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+    case 2048: hipLaunchKernelGGL((col0_solve_kernel<2048>), dim3(1), dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+    case 4096: hipLaunchKernelGGL((col0_solve_kernel<4096>), dim3(1), dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+    default: hipLaunchKernelGGL((col0_solve_kernel<8192>), dim3(1), dim3(Plan<8192>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+  }
+  CFDJ_HIP(hipGetLastError());
 }
 
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st) {

@@ -48,9 +48,12 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
   const int xl = xs == 0 ? nx - 1 : xs - 1;
   const int xr = xs + 2 >= nx ? xs + 2 - nx : xs + 2;
 
-  const int ylim = p.y0 + p.ycount;
-  const int ybeg = p.y0 + (chunk * kWavesPerBlock + wave) * p.rows_per_wave;
-  if (ybeg >= ylim) return;
+  // logical row r0 of the launch: the first window's rows, then the second window's
+  const int r0 = (chunk * kWavesPerBlock + wave) * p.rows_per_wave;
+  if (r0 >= p.ycount + p.ycount_b) return;
+  const bool second = r0 >= p.ycount;
+  const int ylim = second ? p.y0b + p.ycount_b : p.y0 + p.ycount;
+  const int ybeg = second ? p.y0b + (r0 - p.ycount) : p.y0 + r0;
   const int yend = min(ybeg + p.rows_per_wave, ylim);
 
   const StageCoef k = p.k;
@@ -336,7 +339,7 @@ __global__ __launch_bounds__(256) void finite_kernel(const double* __restrict__ 
 // marching kernel.
 static bool stage_tile_ok(const StageParams& p) {
   return !p.march && p.colpart == nullptr && p.nx % kTileCols == 0 &&
-         p.ycount % kTileRows == 0 && p.ycount > 0;
+         p.ycount % kTileRows == 0 && p.ycount > 0 && p.ycount_b == 0;
 }
 
 bool stage_runs_row_group(const StageParams& p) { return stage_tile_ok(p); }
@@ -344,6 +347,10 @@ bool stage_runs_row_group(const StageParams& p) { return stage_tile_ok(p); }
 void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
     throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};
+  if (p.ycount_b != 0 &&
+      (p.ycount_b < 0 || p.y0b < p.y0 + p.ycount || p.y0b + p.ycount_b > p.ny ||
+       p.rows_per_wave < 1 || p.ycount % p.rows_per_wave != 0))
+    throw Error{CFDJ_ERR_ARG, "stage kernel: bad second row window"};
   if (stage_tile_ok(p)) {
     const long blocks = (long)(p.nx / kTileCols) * (p.ycount / kTileRows);
     if (blocks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
@@ -366,9 +373,8 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   }
   const int rpw = p.rows_per_wave;
   const long strips = (p.nx + kColsPerWave - 1) / kColsPerWave;
-  if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
-    throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};
-  const long chunks = (p.ycount + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw);
+  const long chunks =
+      (p.ycount + p.ycount_b + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw);
   if (strips * chunks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
   dim3 grid((unsigned)(strips * chunks));
   dim3 block(kWave * kWavesPerBlock);

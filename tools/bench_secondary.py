@@ -130,11 +130,68 @@ def bench_slabs(steps=3):
     return out
 
 
+def bench_rank_rehearsal(steps=20, single_ms=None):
+    """One rank's compute of an N-rank y-slab step, alone on this GPU (CFDJ_VIRTUAL_SOLO_RANK:
+    rank 0's slab only, every exchange a device copy from itself), launched in the RCCL ranks'
+    own schedule (CFDJ_VIRTUAL_OVERLAP=1: exchanges and the packed column's solve on side
+    streams).  The field is not the global solution -- a timing rehearsal.  `rate_vs_single` =
+    the single-GPU path's time per cell (4096^2, measured here) / this rank's time per cell."""
+    import math
+
+    from cfd_julia_amd import VortexMerger
+    from cfd_julia_amd.common import vm_ic
+
+    def run(nx, ny, P, solo, overlap):
+        dx, dy = 2 * math.pi / nx, 2 * math.pi / ny
+        dt = 5e-4 * 2.0 * 4096.0 ** 2 / (nx * nx + ny * ny)
+        os.environ.pop("CFDJ_VIRTUAL_SOLO_RANK", None)
+        os.environ.pop("CFDJ_VIRTUAL_OVERLAP", None)
+        if solo:
+            os.environ["CFDJ_VIRTUAL_SOLO_RANK"] = "0"
+        if overlap:
+            os.environ["CFDJ_VIRTUAL_OVERLAP"] = "1"
+        kw = dict(kind="virtual", nranks=P) if P else {}
+        with VortexMerger(nx, ny, dx, dy, 1000.0, **kw) as h:
+            row0, rows = h.slab()
+            x, y = dx * np.arange(nx + 1), dy * np.arange(ny + 1)
+            wn = np.zeros((nx + 2, ny + 2), order="F")
+            vm_ic(nx, rows - 1, x, y[row0:], wn[:, row0:])
+            h.upload(wn)
+            del wn
+            h.step(dt, 3)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                h.step(dt, steps)
+                ts.append((time.perf_counter() - t0) / steps)
+            path = h.poisson()
+        os.environ.pop("CFDJ_VIRTUAL_SOLO_RANK", None)
+        os.environ.pop("CFDJ_VIRTUAL_OVERLAP", None)
+        return sorted(ts)[len(ts) // 2] * 1e3, path
+
+    out = []
+    if single_ms is None:
+        single_ms, _ = run(4096, 4096, 0, False, False)
+    per_cell = single_ms / (4096 * 4096)
+    out.append({"config": "R single-GPU path 4096^2", "ms_per_step": round(single_ms, 4)})
+    for ladder, nx, ny, P in (("strong 4096^2", 4096, 4096, 2), ("strong 4096^2", 4096, 4096, 4),
+                              ("strong 4096^2", 4096, 4096, 8),
+                              ("config 5 8192^2", 8192, 8192, 2), ("config 5 8192^2", 8192, 8192, 4),
+                              ("config 5 8192^2", 8192, 8192, 8),
+                              ("weak", 8192, 4096, 2), ("weak", 16384, 8192, 8)):
+        ms, path = run(nx, ny, P, True, True)
+        cells = nx * ny // P
+        out.append({"config": f"R {ladder}: rank 0 of {P}, {nx}x{ny} ({path})",
+                    "cells_per_rank": cells, "ms_per_step": round(ms, 4),
+                    "rate_vs_single": round(per_cell * cells / ms, 3)})
+    return out
+
+
 if __name__ == "__main__":
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--only", default="poisson,cavity,spectral,slabs",
-                    help="comma-separated sections: poisson, cavity, spectral, slabs")
+    ap.add_argument("--only", default="poisson,cavity,spectral,slabs,ranks",
+                    help="comma-separated sections: poisson, cavity, spectral, slabs, ranks")
     a = ap.parse_args()
     only = set(a.only.split(","))
     if "poisson" in only:
@@ -146,4 +203,7 @@ if __name__ == "__main__":
             print(json.dumps(r), flush=True)
     if "slabs" in only:
         for r in bench_slabs():
+            print(json.dumps(r), flush=True)
+    if "ranks" in only:
+        for r in bench_rank_rehearsal(steps=a.steps):
             print(json.dumps(r), flush=True)
