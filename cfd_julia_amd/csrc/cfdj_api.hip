@@ -553,8 +553,7 @@ struct cfdj_vm {
     std::vector<const double*> src(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i)
       src[i] = st == 1 ? slabs[i].wn : st == 2 ? slabs[i].wa : slabs[i].wb;
-    if (slab_mode() && side && !timing && rows % rows_per_wave == 0 &&
-        rows >= 3 * rows_per_wave) {
+    if (slab_mode() && side && !timing && rows >= 3) {
       stage_overlapped(st, dt, src);
       return;
     }
@@ -599,10 +598,9 @@ struct cfdj_vm {
     for (size_t i = 0; i < slabs.size(); ++i) ps[i] = slabs[i].psi;
     halo(true, ps, side);
     CFDJ_HIP(hipEventRecord(ev_shalo, side));
-    // interior blocks first, then -- in one launch -- the first and the last rows_per_wave
-    // rows (which read the halo rows); block-aligned, so the column partials match the
-    // one-launch order
-    const int rb = rows_per_wave;
+    // interior rows first, then -- in one launch -- the first and the last row (which read
+    // the halo rows) adding their values to their blocks' column partials: the stage kernel
+    // sums a block in that order in a one-launch stage as well
     std::vector<StageParams> sp;
     for (size_t i = 0; i < slabs.size(); ++i) {
       Slab& s = slabs[i];
@@ -613,17 +611,18 @@ struct cfdj_vm {
         p.colpart = s.colpart[oi];
         s.cp_valid[oi] = true;
       }
-      p.y0 = rb;
-      p.ycount = rows - 2 * rb;
+      p.y0 = 1;
+      p.ycount = rows - 2;
       launch_stage(st, p, stream);
       sp.push_back(p);
     }
     CFDJ_HIP(hipStreamWaitEvent(stream, ev_shalo, 0));
     for (StageParams& p : sp) {
       p.y0 = 0;
-      p.ycount = rb;
-      p.y0b = rows - rb;
-      p.ycount_b = rb;
+      p.ycount = 1;
+      p.y0b = rows - 1;
+      p.ycount_b = 1;
+      p.cp_accumulate = true;
       launch_stage(st, p, stream);
     }
   }

@@ -141,8 +141,11 @@ struct StageParams {
   int nx, ny;
   int y0, ycount;      // rows [y0, y0 + ycount) of the slab are computed (halo split) ...
   int y0b = 0, ycount_b = 0;  // ... and, in the same launch, rows [y0b, y0b + ycount_b)
-                       // (marching kernel only; both windows whole rows_per_wave blocks)
-  double* colpart;     // optional: per-wave column sums of `out`, [y / rows_per_wave][nx]
+                       // (marching kernel only)
+  int nblk_a = 0, nblk_b = 0;  // set by launch_stage: rows_per_wave blocks each window touches
+  bool cp_accumulate = false;  // colpart: add to the stored partial instead of replacing it
+  double* colpart;     // optional: column sums of `out` per block of rows_per_wave rows,
+                       // [y / rows_per_wave][nx] (increasing row order, the slab's row 0 last)
   int rows_per_wave;
   bool march;          // true: always the marching kernel (rows_per_wave rows per wavefront)
   StageCoef k;

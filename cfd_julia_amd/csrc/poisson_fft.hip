@@ -23,6 +23,7 @@
 // contraction is allowed here: the FFT is not bit-comparable to FFTW / pocketfft anyway
 // (tolerance 1e-12 relative on psi, tests/test_gpu_parity.py).
 #pragma clang fp contract(fast)
+#include <cstdlib>
 #include <type_traits>
 
 #include "fft_lds.hpp"
@@ -760,6 +761,16 @@ static int persistent_grid(int ncu, int per_cu, int items) {
 template <int L, bool FWD>
 void launch_rows_dir(int pass, const FusedPoissonArgs& a, hipStream_t st);
 
+// CFDJ_FWD_NP=2|4|8 (read once): see launch_rows.
+static int fwd_np_rows() {
+  static const int v = [] {
+    const char* e = std::getenv("CFDJ_FWD_NP");
+    const int x = e ? std::atoi(e) : 0;
+    return x == 2 || x == 4 || x == 8 ? x : 0;
+  }();
+  return v;
+}
+
 template <int L>
 void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
 #if CFDJ_ROWS_INV_NP > 0
@@ -794,6 +805,29 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
         }
         return;
       }
+    } else if (pass == 0 && L <= 2048 && fwd_np_rows() > 0) {
+      // A/B switch (CFDJ_FWD_NP=2|4|8): the forward pass in the small-item shape on the
+      // column-major layout, XR rows per workgroup (column segments of 16 XR bytes)
+      const int xr = fwd_np_rows();
+      auto go = [&](auto xrc) {
+        constexpr int XR = decltype(xrc)::value;
+        if constexpr (XR * Plan<L>::T <= 1024) {
+          if (a.rows % XR != 0) throw Error{CFDJ_ERR_ARG, "CFDJ_FWD_NP: rows not a multiple"};
+          const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
+          if (a.stream)
+            hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, false, true>), grid, block, 0, st, a.f,
+                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr);
+          else
+            hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, false, false>), grid, block, 0, st, a.f,
+                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr);
+        } else {
+          throw Error{CFDJ_ERR_ARG, "CFDJ_FWD_NP: workgroup too large for this row length"};
+        }
+      };
+      if (xr == 2) go(std::integral_constant<int, 2>{});
+      else if (xr == 4) go(std::integral_constant<int, 4>{});
+      else go(std::integral_constant<int, 8>{});
+      return;
     } else if (pass != 0 && L <= 2048) {
       constexpr int XR = rows_np_xr<L, false>();
       if (a.rows % XR == 0) {

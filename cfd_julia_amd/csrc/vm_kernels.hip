@@ -48,13 +48,25 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
   const int xl = xs == 0 ? nx - 1 : xs - 1;
   const int xr = xs + 2 >= nx ? xs + 2 - nx : xs + 2;
 
-  // logical row r0 of the launch: the first window's rows, then the second window's
-  const int r0 = (chunk * kWavesPerBlock + wave) * p.rows_per_wave;
-  if (r0 >= p.ycount + p.ycount_b) return;
-  const bool second = r0 >= p.ycount;
-  const int ylim = second ? p.y0b + p.ycount_b : p.y0 + p.ycount;
-  const int ybeg = second ? p.y0b + (r0 - p.ycount) : p.y0 + r0;
-  const int yend = min(ybeg + p.rows_per_wave, ylim);
+  // A wavefront takes the part of ONE block of rows_per_wave rows (blocks are absolute: block
+  // b = rows [b rpw, (b+1) rpw)) that lies in a window of the launch: the blocks the first
+  // window touches, then those of the second.
+  const int wi = chunk * kWavesPerBlock + wave;
+  const int rpw = p.rows_per_wave;
+  int blk, wy0, wy1;
+  if (wi < p.nblk_a) {
+    blk = p.y0 / rpw + wi;
+    wy0 = p.y0;
+    wy1 = p.y0 + p.ycount;
+  } else if (wi < p.nblk_a + p.nblk_b) {
+    blk = p.y0b / rpw + (wi - p.nblk_a);
+    wy0 = p.y0b;
+    wy1 = p.y0b + p.ycount_b;
+  } else {
+    return;
+  }
+  const int ybeg = max(wy0, blk * rpw);
+  const int yend = min(wy1, (blk + 1) * rpw);
 
   const StageCoef k = p.k;
   Raw wr_p = fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg + 1, ny, nx), xs, xl, xr, is_l, is_r);
@@ -64,7 +76,12 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
   Win wc = expand(fetch(row_ptr(p.w, p.w_lo, p.w_hi, ybeg, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
   Win sc = expand(fetch(row_ptr(p.s, p.s_lo, p.s_hi, ybeg, ny, nx), xs, xl, xr, is_l, is_r), is_l, is_r);
 
-  double2 csum = make_double2(0.0, 0.0);  // this wave's column sums of `out` (colpart)
+  // Column sums of `out` over the block (colpart).  Their order is fixed so that a slab
+  // computed in one launch and one computed as interior rows + the first and the last row
+  // (the rows that read the halo rows) agree to the bit: row 0 of the slab is added LAST to
+  // its block's sum, every other row in increasing order.
+  double2 csum = make_double2(0.0, 0.0), held = csum;
+  const bool hold = p.colpart != nullptr && ybeg == 0 && yend > 1;
   for (int y = ybeg; y < yend; ++y) {
     // prefetch row y+2 (clamped: the last iteration re-reads row yend, harmlessly)
     const int yn = min(y + 2, yend);
@@ -85,8 +102,12 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
     // (streamed on large slabs: 1.3 % of the y-slab step; in the row-group kernel the same
     // brought nothing beyond what the streaming store of psi already gives)
     if (valid) store_stream<NT>(reinterpret_cast<double2*>(p.out + (size_t)y * nx + xs), o);
-    csum.x += o.x;
-    csum.y += o.y;
+    if (hold && y == 0) {
+      held = o;
+    } else {
+      csum.x += o.x;
+      csum.y += o.y;
+    }
 
     wm = wc;
     wc = wp;
@@ -95,8 +116,19 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
     wr_p = wr_n;
     sr_p = sr_n;
   }
-  if (p.colpart != nullptr && valid)
-    *reinterpret_cast<double2*>(p.colpart + (size_t)(ybeg / p.rows_per_wave) * nx + xs) = csum;
+  if (p.colpart != nullptr && valid) {
+    double2* cp = reinterpret_cast<double2*>(p.colpart + (size_t)blk * nx + xs);
+    if (hold) {
+      csum.x += held.x;
+      csum.y += held.y;
+    }
+    if (p.cp_accumulate) {  // the rest of the block came from an earlier launch
+      const double2 prev = *cp;
+      csum.x = prev.x + csum.x;
+      csum.y = prev.y + csum.y;
+    }
+    *cp = csum;
+  }
 }
 
 // Row-group variant of the stage kernel: a 256-thread workgroup owns 512 consecutive x of
@@ -227,7 +259,7 @@ __global__ __launch_bounds__(256) CFDJ_TILE_ATTR void vm_stage_tile_kernel(const
 }
 
 // colpart[b][x] = sum over rows [b rpw, (b+1) rpw) of f[y][x], in the row order of the
-// stage kernel's csum (so a field gets the same partials either way).
+// stage kernel's csum (increasing, row 0 last), so a field gets the same partials either way.
 __global__ __launch_bounds__(256) void colpart_kernel(const double* __restrict__ f, int nx,
                                                       int rows, int rpw,
                                                       double* __restrict__ colpart) {
@@ -236,7 +268,8 @@ __global__ __launch_bounds__(256) void colpart_kernel(const double* __restrict__
   if (x >= nx) return;
   double s = 0.0;
   const int y1 = min((b + 1) * rpw, rows);
-  for (int y = b * rpw; y < y1; ++y) s += f[(size_t)y * nx + x];
+  for (int y = max(b * rpw, 1); y < y1; ++y) s += f[(size_t)y * nx + x];
+  if (b == 0) s += f[x];  // row 0 last (the stage kernel's order)
   colpart[(size_t)b * nx + x] = s;
 }
 
@@ -348,8 +381,7 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
     throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};
   if (p.ycount_b != 0 &&
-      (p.ycount_b < 0 || p.y0b < p.y0 + p.ycount || p.y0b + p.ycount_b > p.ny ||
-       p.rows_per_wave < 1 || p.ycount % p.rows_per_wave != 0))
+      (p.ycount_b < 0 || p.y0b < p.y0 + p.ycount || p.y0b + p.ycount_b > p.ny))
     throw Error{CFDJ_ERR_ARG, "stage kernel: bad second row window"};
   if (stage_tile_ok(p)) {
     const long blocks = (long)(p.nx / kTileCols) * (p.ycount / kTileRows);
@@ -372,25 +404,29 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
     return;
   }
   const int rpw = p.rows_per_wave;
+  if (rpw < 1) throw Error{CFDJ_ERR_ARG, "stage kernel: rows per wavefront must be >= 1"};
   const long strips = (p.nx + kColsPerWave - 1) / kColsPerWave;
-  const long chunks =
-      (p.ycount + p.ycount_b + kWavesPerBlock * rpw - 1) / (kWavesPerBlock * rpw);
+  // blocks of rpw rows (absolute) that each window touches: one wavefront per block and strip
+  StageParams q = p;
+  q.nblk_a = (p.y0 + p.ycount - 1) / rpw - p.y0 / rpw + 1;
+  q.nblk_b = p.ycount_b > 0 ? (p.y0b + p.ycount_b - 1) / rpw - p.y0b / rpw + 1 : 0;
+  const long chunks = (q.nblk_a + q.nblk_b + kWavesPerBlock - 1) / kWavesPerBlock;
   if (strips * chunks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
   dim3 grid((unsigned)(strips * chunks));
   dim3 block(kWave * kWavesPerBlock);
   switch (stage) {
-    case 0: hipLaunchKernelGGL((vm_stage_kernel<0, false>), grid, block, 0, st, p); break;
+    case 0: hipLaunchKernelGGL((vm_stage_kernel<0, false>), grid, block, 0, st, q); break;
     case 1:
-      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<1, true>), grid, block, 0, st, p);
-      else hipLaunchKernelGGL((vm_stage_kernel<1, false>), grid, block, 0, st, p);
+      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<1, true>), grid, block, 0, st, q);
+      else hipLaunchKernelGGL((vm_stage_kernel<1, false>), grid, block, 0, st, q);
       break;
     case 2:
-      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<2, true>), grid, block, 0, st, p);
-      else hipLaunchKernelGGL((vm_stage_kernel<2, false>), grid, block, 0, st, p);
+      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<2, true>), grid, block, 0, st, q);
+      else hipLaunchKernelGGL((vm_stage_kernel<2, false>), grid, block, 0, st, q);
       break;
     default:
-      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<3, true>), grid, block, 0, st, p);
-      else hipLaunchKernelGGL((vm_stage_kernel<3, false>), grid, block, 0, st, p);
+      if (p.stream) hipLaunchKernelGGL((vm_stage_kernel<3, true>), grid, block, 0, st, q);
+      else hipLaunchKernelGGL((vm_stage_kernel<3, false>), grid, block, 0, st, q);
       break;
   }
   CFDJ_HIP(hipGetLastError());
