@@ -301,6 +301,26 @@ void launch_half_r2c2d(const HalfSpecArgs& a, const double* r, double2* scratch,
 void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, double2* x, double* r,
                        hipStream_t st);
 
+// 2-D transforms of REAL n-by-n fields with n = 3 * 2^k (1536, 3072, 6144: the 3/2 rule's
+// product grids) on the columns m = 0..mmax of the half spectrum (fft2d_r2c3.hip): element
+// (m, k) at m n + k (ky contiguous); the spectrum is zero / not wanted beyond column mmax
+// (mmax < n/2), slot (0, .) holds the DC column alone.  Unnormalised both ways.
+struct Real2d3Args {
+  int n;                 // grid size
+  int mmax;              // last kx column held
+  const double2* tw3L;   // exp(-2 pi i k/(n/6)): the row transforms' power-of-two thirds
+  const double2* twL;    // exp(-2 pi i k/(n/2))
+  const double2* twN;    // exp(-2 pi i k/n)
+  const double2* tw3M;   // exp(-2 pi i k/(n/3)): the column transforms' thirds
+  bool stream;           // once-read / once-written real fields by streaming loads / stores
+};
+bool real2d3_supported(int n);
+// r[b] = real(ifft2(x[b])) n n for b < batch; x: batch x (mmax + 1) x n complex, transformed
+// in place along y on the way.
+void launch_c2r2d3(const Real2d3Args& a, double2* x, double* r, int batch, hipStream_t st);
+// x = columns 0..mmax of fft2(r).
+void launch_r2c2d3(const Real2d3Args& a, const double* r, double2* x, hipStream_t st);
+
 // Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row
 // per rank (row 0 of each slab); interior blocks by DST-I (odd-extension FFT of length

@@ -1,0 +1,367 @@
+// 2-D real <-> half-spectrum transforms on grids of 3 * 2^k points a side (1536, 3072, 6144):
+// the product grid of the 3/2-rule solver (21_NS2D_PseudoSpectral_32_Rule/
+// pseudospectral_32_rule.jl:124-125 pads nx to 1.5 nx), which the power-of-two passes of
+// poisson_fft.hip / fft2d_r2c.hip do not cover.
+//
+// A transform of length L = 3 L3 (L3 a power of two) is three independent length-L3 Stockham
+// transforms (the radix-16 plans of fft_lds.hpp) of the decimated inputs x[3 n + r], one per
+// third of the workgroup's team, followed by ONE decimation-in-time radix-3 step: X[k + q L3]
+// = F_0[k] + W_L^p F_1[k] + W_L^2p F_2[k], p = k + q L3.  The team's LDS buffer holds one
+// double per element (real and imaginary parts pass through it one after the other, as in
+// the column pass of the Poisson solver): it serves as the three sub-transforms' exchange
+// buffers, as the exchange of the radix-3 step (each thread reads the three F_r[k] of its 16
+// outputs and accumulates them component by component -- the step is linear), and as the
+// natural-order buffer of the (m, L - m) pairs of the real-transform pre/post-processing.
+//
+// Layout of the half spectrum between the passes: column-major, element (m, y) at m n + y
+// (ky contiguous), columns m = 0 .. mmax only -- the padded spectrum is zero beyond the
+// unpadded grid's Nyquist column, so neither pass touches those columns.  Slot 0 of a row's
+// packed spectrum holds X[0] alone: the padded grid's own Nyquist mode is zero on the way in
+// and dropped on the way out (pseudospectral_32_rule.jl:171-178 does not unpad it).
+//
+// Both directions are unnormalised, like the library transforms they stand in for.
+#pragma clang fp contract(fast)
+#include "fft_lds.hpp"
+
+namespace cfdj {
+
+namespace {
+
+template <int L3>
+struct Cfg3 {
+  static constexpr int L = 3 * L3;
+  static constexpr int T3 = Plan<L3>::T;       // threads per sub-transform
+  static constexpr int TT = 3 * T3;            // threads per transform (team)
+  static constexpr int PAD3 = Plan<L3>::PAD;   // doubles per sub-transform buffer
+  static constexpr int PADL = 3 * PAD3;        // doubles per team buffer (>= padx(L - 1) + 1)
+  static_assert(Plan<L3>::NSTAGES >= 2 && Plan<L3>::radix(0) == 16, "sub-transform length");
+};
+
+// The sub-transform of branch q on its decimated inputs in v (v[r] = x[3 (tid + T3 r) + q]);
+// on return v holds F_q[k] at the last stage's output positions k.
+template <int L3, int DIR>
+__device__ __forceinline__ void sub_fft(double* team_buf, double2 (&v)[16], int q, int tid,
+                                        const double2* __restrict__ tw3_) {
+  const TwGlobal<L3> tw3{tw3_};
+  stage_regs<L3, 0, DIR>(v, tid, tw3);
+  run_stages_half<L3, 1, DIR>(team_buf + q * Cfg3<L3>::PAD3, v, tid, tw3);
+}
+
+// The radix-3 step: the three sub-transforms' outputs F_r[k] (in v, r = q) -> out[j] =
+// X[p], p = k + q L3, k = tid + T3 j: a thread's outputs are contiguous in p across the
+// lanes of its sub-team.  The F_r go through the team buffer one component at a time (F_r[k]
+// at r L3 + k); X[p] = F_0 + c1 F_1 + c2 F_2 with c1 = W_L^p, c2 = W_L^2p (conjugated for the
+// inverse), accumulated per component.
+template <int L3, int DIR>
+__device__ __forceinline__ void combine3(double* team_buf, const double2 (&v)[16], int q,
+                                         int tid, const double2* __restrict__ twL,
+                                         double2 (&out)[16]) {
+  using C = Cfg3<L3>;
+  using P = Plan<L3>;
+  constexpr int SL = P::NSTAGES - 1;
+  constexpr int RL = P::radix(SL);
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();  // the buffer's previous readers
+#pragma unroll
+    for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+      for (int r = 0; r < RL; ++r)
+        team_buf[padx(q * L3 + out_pos<L3, SL>(tid, b, r))] = c ? v[b * RL + r].y : v[b * RL + r].x;
+    __syncthreads();
+    // an opaque copy of the thread index per component: the twiddles are loaded again in the
+    // second pass instead of staying live (64 registers) across the exchange
+    int tk = tid;
+    asm volatile("" : "+v"(tk));
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = tk + C::T3 * j;
+      const int p = k + q * L3;
+      double2 c1 = twL[p];
+      if (DIR > 0) c1.y = -c1.y;
+      const double2 c2 = cmul(c1, c1);
+      const double f0 = team_buf[padx(k)], f1 = team_buf[padx(L3 + k)],
+                   f2 = team_buf[padx(2 * L3 + k)];
+      if (c == 0) {
+        out[j] = make_double2(f0 + f1 * c1.x + f2 * c2.x, f1 * c1.y + f2 * c2.y);
+      } else {  // i f c = (-f c.y, f c.x)
+        out[j].x -= f1 * c1.y + f2 * c2.y;
+        out[j].y += f0 + f1 * c1.x + f2 * c2.x;
+      }
+    }
+  }
+}
+
+// ---- columns: one contiguous column of M = 3 M3 elements per workgroup, in place -----------
+#ifndef CFDJ_COLS3_WAVES
+#define CFDJ_COLS3_WAVES 4  // > 0: wavefronts per SIMD the kernel is compiled for
+#endif
+#if CFDJ_COLS3_WAVES > 0
+#define CFDJ_COLS3_ATTR __attribute__((amdgpu_waves_per_eu(CFDJ_COLS3_WAVES, CFDJ_COLS3_WAVES)))
+#else
+#define CFDJ_COLS3_ATTR
+#endif
+template <int M3, int DIR>
+__global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_kernel(
+    double2* __restrict__ data, const double2* __restrict__ tw3,
+    const double2* __restrict__ twM) {
+  using C = Cfg3<M3>;
+  __shared__ double lds[C::PADL];
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  double2* col = data + (size_t)id * C::L;
+  const int t = threadIdx.x, q = t / C::T3, tid = t % C::T3;
+  double2 v[16];
+  // the three sub-teams' loads interleave element by element: together whole lines
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = col[3 * (tid + C::T3 * r) + q];
+  sub_fft<M3, DIR>(lds, v, q, tid, tw3);
+  double2 o[16];
+  combine3<M3, DIR>(lds, v, q, tid, twM, o);
+  // (the DC column of a real field's spectrum transforms to real values up to round-off; the
+  // inverse row pass reads the real parts of column 0 only)
+#pragma unroll
+  for (int j = 0; j < 16; ++j) col[tid + C::T3 * j + q * M3] = o[j];
+}
+
+// Pair i of a thread in a row workgroup of XR teams: row qq, columns m and L - m; 16
+// consecutive lanes take 16 consecutive m of one row (whole XR * 16-B column segments).
+template <int L3, int XR>
+__device__ __forceinline__ void pair3(int i, int& qq, int& m) {
+  const int e = threadIdx.x + i * (XR * Cfg3<L3>::TT);
+  qq = (e >> 4) % XR;
+  m = ((e >> 4) / XR) * 16 + (e & 15);
+}
+
+// ---- rows, half spectrum -> real (c2r): XR rows per workgroup ------------------------------
+#ifndef CFDJ_ROWS3_INV_WAVES
+#define CFDJ_ROWS3_INV_WAVES 4  // > 0: wavefronts per SIMD the kernel is compiled for
+#endif
+#if CFDJ_ROWS3_INV_WAVES > 0
+#define CFDJ_ROWS3_INV_ATTR \
+  __attribute__((amdgpu_waves_per_eu(CFDJ_ROWS3_INV_WAVES, CFDJ_ROWS3_INV_WAVES)))
+#else
+#define CFDJ_ROWS3_INV_ATTR
+#endif
+template <int L3, int XR, bool NTS>
+__global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_inv_kernel(
+    const double2* __restrict__ H, double* __restrict__ f, int M, int mmax,
+    const double2* __restrict__ tw3, const double2* __restrict__ twL,
+    const double2* __restrict__ twN) {
+  using C = Cfg3<L3>;
+  constexpr int L = C::L, THREADS = XR * C::TT, PAIRS = (L / 2) * XR / THREADS;
+  static_assert(PAIRS * THREADS == (L / 2) * XR, "pair mapping");
+  __shared__ double lds[XR * C::PADL];
+  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  double* buf = lds + team * C::PADL;
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  const double2* base = H + __builtin_amdgcn_readfirstlane(y0);
+  // c2r pre-processing of the pairs (m, L - m): Z[m] = (X[m] + conj X[L-m]) + i W_N^-m (X[m] -
+  // conj X[L-m]); slot 0 = X[0] (the Nyquist mode of this grid is zero), Z[L/2] = 2 conj X[L/2]
+  double2 o1[PAIRS], o2[PAIRS];
+#pragma unroll
+  for (int i = 0; i < PAIRS; ++i) {
+    int qq, m;
+    pair3<L3, XR>(i, qq, m);
+    const bool z0 = i == 0 && m == 0;
+    const int mq = z0 ? L / 2 : L - m;
+    double2 Xm = make_double2(0.0, 0.0), Xq = Xm;
+    if (m <= mmax) Xm = base[(size_t)m * M + qq];
+    if (mq <= mmax) Xq = base[(size_t)mq * M + qq];
+    const double2 Xp = cconj(Xq);
+    const double2 S = cadd(Xm, Xp);
+    const double2 D = cmul(cconj(twN[m]), csub(Xm, Xp));
+    o1[i] = make_double2(S.x - D.y, S.y + D.x);
+    o2[i] = make_double2(S.x + D.y, D.x - S.y);
+    if (z0) {
+      o1[i] = make_double2(Xm.x, Xm.x);  // (X[0] + X[L], X[0] - X[L]) with X[L] = 0
+      o2[i] = make_double2(2.0 * Xq.x, -2.0 * Xq.y);
+    }
+  }
+  // through the natural-order buffer one component at a time, read back as the
+  // sub-transforms' decimated inputs
+  double2 v[16];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    if (c) __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      int qq, m;
+      pair3<L3, XR>(i, qq, m);
+      double* bq = lds + qq * C::PADL;
+      bq[padx(m)] = c ? o1[i].y : o1[i].x;
+      bq[padx(i == 0 && m == 0 ? L / 2 : L - m)] = c ? o2[i].y : o2[i].x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const double a = buf[padx(3 * (tid + C::T3 * r) + q)];
+      if (c) v[r].y = a;
+      else v[r].x = a;
+    }
+  }
+  sub_fft<L3, 1>(buf, v, q, tid, tw3);
+  double2 o[16];
+  combine3<L3, 1>(buf, v, q, tid, twL, o);
+  double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + team) * (2 * L));
+#pragma unroll
+  for (int j = 0; j < 16; ++j) store_stream<NTS>(z + tid + C::T3 * j + q * L3, o[j]);
+}
+
+// ---- rows, real -> half spectrum (r2c): XR rows per workgroup ------------------------------
+template <int L3, int XR, bool NT>
+__global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_fwd_kernel(
+    const double* __restrict__ f, double2* __restrict__ H, int M, int mmax,
+    const double2* __restrict__ tw3, const double2* __restrict__ twL,
+    const double2* __restrict__ twN) {
+  using C = Cfg3<L3>;
+  constexpr int L = C::L, THREADS = XR * C::TT, PAIRS = (L / 2) * XR / THREADS;
+  __shared__ double lds[XR * C::PADL];
+  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  double* buf = lds + team * C::PADL;
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  const double2* z = reinterpret_cast<const double2*>(f) + (size_t)(y0 + team) * L;
+  double2 v[16];
+  // the three sub-teams' loads interleave element by element: together whole lines
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = load_stream<NT>(z + 3 * (tid + C::T3 * r) + q);
+  sub_fft<L3, -1>(buf, v, q, tid, tw3);
+  double2 o[16];
+  combine3<L3, -1>(buf, v, q, tid, twL, o);
+  // natural order through the buffer, read back as the pairs (m, L - m) of the r2c
+  // post-processing
+  double2 Zm[PAIRS], Zp[PAIRS];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < 16; ++j) buf[padx(tid + C::T3 * j + q * L3)] = c ? o[j].y : o[j].x;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      int qq, m;
+      pair3<L3, XR>(i, qq, m);
+      const double* bq = lds + qq * C::PADL;
+      const double a = bq[padx(m)], b = bq[padx(i == 0 && m == 0 ? L / 2 : L - m)];
+      if (c) {
+        Zm[i].y = a;
+        Zp[i].y = b;
+      } else {
+        Zm[i].x = a;
+        Zp[i].x = b;
+      }
+    }
+  }
+  double2* hb = H + __builtin_amdgcn_readfirstlane(y0);
+#pragma unroll
+  for (int i = 0; i < PAIRS; ++i) {
+    int qq, m;
+    pair3<L3, XR>(i, qq, m);
+    const bool z0 = i == 0 && m == 0;
+    const int mp = z0 ? L / 2 : L - m;
+    const double2 Zc = cconj(Zp[i]);
+    const double2 E = make_double2(0.5 * (Zm[i].x + Zc.x), 0.5 * (Zm[i].y + Zc.y));
+    const double2 D = csub(Zm[i], Zc);
+    const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);
+    const double2 WO = cmul(twN[m], O);
+    double2 o1 = cadd(E, WO);
+    double2 o2 = cconj(csub(E, WO));
+    if (z0) {  // slot 0 = X[0] (this grid's Nyquist mode X[L] is not kept); X[L/2] = conj Z[L/2]
+      o1 = make_double2(Zm[i].x + Zm[i].y, 0.0);
+      o2 = Zc;
+    }
+    if (m <= mmax) hb[(size_t)m * M + qq] = o1;
+    if (mp <= mmax) hb[(size_t)mp * M + qq] = o2;
+  }
+}
+
+// Rows per workgroup.  Measured at 6144^2 (4 steps of the 3/2-rule solver at 4096^2, rocprofv3):
+// the inverse pass takes 200 us per array with 1, 2 or 4 rows; the forward pass 275 / 272 /
+// 217 us -- its column segments are written, and 64-B pieces (4 rows) merge better.
+#ifndef CFDJ_ROWS3_XR
+#define CFDJ_ROWS3_XR 2
+#endif
+#ifndef CFDJ_ROWS3_FWD_XR
+#define CFDJ_ROWS3_FWD_XR 4
+#endif
+
+template <int L3>
+void launch_rows3(bool fwd, const Real2d3Args& a, const double* fin, double* fout, double2* H,
+                  hipStream_t st) {
+  constexpr int XR = CFDJ_ROWS3_XR;
+  const dim3 grid(a.n / XR), block(XR * Cfg3<L3>::TT);
+  if (fwd) {
+    constexpr int XF = CFDJ_ROWS3_FWD_XR * Cfg3<L3>::TT <= 1024 ? CFDJ_ROWS3_FWD_XR : XR;
+    const dim3 gridf(a.n / XF), blockf(XF * Cfg3<L3>::TT);
+    if (a.stream)
+      hipLaunchKernelGGL((rows3_fwd_kernel<L3, XF, true>), gridf, blockf, 0, st, fin, H, a.n,
+                         a.mmax, a.tw3L, a.twL, a.twN);
+    else
+      hipLaunchKernelGGL((rows3_fwd_kernel<L3, XF, false>), gridf, blockf, 0, st, fin, H, a.n,
+                         a.mmax, a.tw3L, a.twL, a.twN);
+  } else {
+    if (a.stream)
+      hipLaunchKernelGGL((rows3_inv_kernel<L3, XR, true>), grid, block, 0, st, H, fout, a.n,
+                         a.mmax, a.tw3L, a.twL, a.twN);
+    else
+      hipLaunchKernelGGL((rows3_inv_kernel<L3, XR, false>), grid, block, 0, st, H, fout, a.n,
+                         a.mmax, a.tw3L, a.twL, a.twN);
+  }
+}
+
+template <int M3>
+void launch_cols3(bool fwd, const Real2d3Args& a, double2* x, int batch, hipStream_t st) {
+  const int ncols = a.mmax + 1;
+  const dim3 grid((unsigned)(ncols * batch)), block(Cfg3<M3>::TT);
+  if (fwd) hipLaunchKernelGGL((cols3_kernel<M3, -1>), grid, block, 0, st, x, a.tw3M, a.twN);
+  else hipLaunchKernelGGL((cols3_kernel<M3, 1>), grid, block, 0, st, x, a.tw3M, a.twN);
+}
+
+void check3(const Real2d3Args& a) {
+  if (!real2d3_supported(a.n) || a.mmax < 0 || a.mmax >= a.n / 2 || a.n % CFDJ_ROWS3_XR != 0 ||
+      a.n % CFDJ_ROWS3_FWD_XR != 0)
+    throw Error{CFDJ_ERR_ARG, "3 * 2^k transform: unsupported size"};
+}
+
+}  // namespace
+
+bool real2d3_supported(int n) { return n == 1536 || n == 3072 || n == 6144; }
+
+void launch_c2r2d3(const Real2d3Args& a, double2* x, double* r, int batch, hipStream_t st) {
+  check3(a);
+  const size_t half = (size_t)(a.mmax + 1) * a.n, full = (size_t)a.n * a.n;
+  switch (a.n) {
+    case 1536: launch_cols3<512>(false, a, x, batch, st); break;
+    case 3072: launch_cols3<1024>(false, a, x, batch, st); break;
+    default: launch_cols3<2048>(false, a, x, batch, st); break;
+  }
+  CFDJ_HIP(hipGetLastError());
+  for (int b = 0; b < batch; ++b) {
+    switch (a.n) {
+      case 1536: launch_rows3<256>(false, a, nullptr, r + b * full, x + b * half, st); break;
+      case 3072: launch_rows3<512>(false, a, nullptr, r + b * full, x + b * half, st); break;
+      default: launch_rows3<1024>(false, a, nullptr, r + b * full, x + b * half, st); break;
+    }
+    CFDJ_HIP(hipGetLastError());
+  }
+}
+
+void launch_r2c2d3(const Real2d3Args& a, const double* r, double2* x, hipStream_t st) {
+  check3(a);
+  switch (a.n) {
+    case 1536:
+      launch_rows3<256>(true, a, r, nullptr, x, st);
+      launch_cols3<512>(true, a, x, 1, st);
+      break;
+    case 3072:
+      launch_rows3<512>(true, a, r, nullptr, x, st);
+      launch_cols3<1024>(true, a, x, 1, st);
+      break;
+    default:
+      launch_rows3<1024>(true, a, r, nullptr, x, st);
+      launch_cols3<2048>(true, a, x, 1, st);
+      break;
+  }
+  CFDJ_HIP(hipGetLastError());
+}
+
+}  // namespace cfdj

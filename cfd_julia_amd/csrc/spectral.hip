@@ -360,6 +360,82 @@ __global__ void ps32_derivs_half_kernel(const double2* __restrict__ wf,
   }
 }
 
+// The same four spectra in the column layout of the hand-written 3 * 2^k transforms
+// (fft2d_r2c3.hip): columns a = 0..nx/2 only (beyond, the padded spectrum is zero), element
+// (a, b) of array q at (q (nx/2 + 1) + a) py + b, ky contiguous.  w_f is read along kx and the
+// result written along ky, through a 16 x 16 tile in LDS; one 256-thread workgroup per tile,
+// grid = (ceil((nx/2 + 1) / 16), py / 16).
+__global__ __launch_bounds__(256) void ps32_derivs_cols_kernel(
+    const double2* __restrict__ wf, const double* __restrict__ kx, double2* __restrict__ D,
+    int nx, int ny, int px, int py, double sc, double sd) {
+  __shared__ double2 tile[4][16][17];
+  const int hx = nx / 2, hy = ny / 2, qx = px - hx, qy = py - hy, ncol = hx + 1;
+  const int ta = threadIdx.x & 15, tb = threadIdx.x >> 4;
+  const int a0 = blockIdx.x * 16 + ta, b0 = blockIdx.y * 16 + tb;
+  double2 acc[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) acc[q] = make_double2(0.0, 0.0);
+  if (a0 < ncol) {
+#pragma unroll
+    for (int side = 0; side < 2; ++side) {
+      const int a = side ? (a0 == 0 ? 0 : px - a0) : a0, b = side ? (b0 == 0 ? 0 : py - b0) : b0;
+      if (!((a < hx || a >= qx) && (b < hy || b >= qy))) continue;
+      const int i = a < hx ? a : a - qx + hx, j = b < hy ? b : b - qy + hy;
+      const double kxi = kx[i], kyj = kx[j];
+      const double k2 = kxi * kxi + kyj * kyj;
+      const double2 iw = times_i(wf[(size_t)j * nx + i]);
+      double2 d[4];
+      d[0] = cdiv_r(cmul_r(kxi, iw), k2);  // 1im * wf * kx / k2
+      d[1] = cmul_r(kyj, iw);              // 1im * wf * ky
+      d[2] = cdiv_r(cmul_r(kyj, iw), k2);  // 1im * wf * ky / k2
+      d[3] = cmul_r(kxi, iw);              // 1im * wf * kx
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const double2 p = make_double2(d[q].x * sc / sd, d[q].y * sc / sd);
+        acc[q].x += 0.5 * p.x;
+        acc[q].y += side ? -0.5 * p.y : 0.5 * p.y;
+      }
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) tile[q][ta][tb] = acc[q];
+  __syncthreads();
+  const int wa = blockIdx.x * 16 + tb, wb = blockIdx.y * 16 + ta;  // ky fastest on the way out
+  if (wa < ncol) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+      D[((size_t)q * ncol + wa) * py + wb] = tile[q][tb][ta];
+  }
+}
+
+// pseudospectral_32_rule.jl:171-178 from the columns 0..nx/2 of the product's spectrum in that
+// layout (Jc, element (a, b) at a py + b): jf(i, j) = fft(product)(a, b) (nx ny) / (nxe nye);
+// kx indices i >= nx/2 are the conjugates of (-a, -b).  Read along ky, written along kx
+// through a 16 x 16 tile; grid = (nx / 16, ny / 16).
+__global__ __launch_bounds__(256) void ps32_unpad_cols_kernel(const double2* __restrict__ Jc,
+                                                              double2* __restrict__ jf, int nx,
+                                                              int ny, int px, int py, double sd,
+                                                              double sc) {
+  __shared__ double2 tile[16][17];
+  const int hx = nx / 2, hy = ny / 2;
+  const int tj = threadIdx.x & 15, ti = threadIdx.x >> 4;  // ky fastest on the way in
+  {
+    const int i = blockIdx.x * 16 + ti, j = blockIdx.y * 16 + tj;
+    const int a = i < hx ? i : i - hx + (px - hx), b = j < hy ? j : j - hy + (py - hy);
+    double2 v;
+    if (i < hx) {
+      v = Jc[(size_t)a * py + b];
+    } else {
+      v = Jc[(size_t)(px - a) * py + (b == 0 ? 0 : py - b)];
+      v.y = -v.y;
+    }
+    tile[ti][tj] = make_double2(v.x * sd / sc, v.y * sd / sc);
+  }
+  __syncthreads();
+  const int wi = blockIdx.x * 16 + tj, wj = blockIdx.y * 16 + ti;
+  jf[(size_t)wj * nx + wi] = tile[tj][ti];
+}
+
 // pseudospectral_32_rule.jl:171-178 from the half spectrum Jh ((px/2 + 1) x py) of the real
 // product: jf(i, j) = fft(product)(a, b) * (nx ny) / (nxe nye), (a, b) the padded index of
 // mode (i, j); a > px/2 is the conjugate of (-a, -b).
@@ -440,10 +516,14 @@ __global__ void to_field_real_kernel(const double* __restrict__ R, double* __res
 }
 
 // Full spectrum (nx x ny, kx contiguous) <-> half spectrum ((nx/2 + 1) columns of ny, ky
-// contiguous) of a real field: the other half is conj(w_f(-kx, -ky)).  The import keeps the
-// Hermitian part (w_f(k) + conj(w_f(-k))) / 2 of whatever it is given -- the part the
-// reference's jacobian() sees through real(ifft(.)) (hybrid.jl:103,115) -- so a spectrum
-// that is not that of a real field gives the same Jacobian here as on the full-spectrum path.
+// contiguous) of a real field: the other half is conj(w_f(-kx, -ky)).  HERM: the import keeps
+// the Hermitian part (w_f(k) + conj(w_f(-k))) / 2 of whatever it is given -- all that
+// hybrid.jl's jacobian() sees of w_f through real(ifft(w_f)) and real(ifft(w_f / k2))
+// (hybrid.jl:103,115; k2 is even) -- so a spectrum that is not that of a real field gives the
+// reference's Jacobian.  The pseudospectral rules multiply by i k and a band filter that are
+// not Hermitian at index 1 (kx[1] = eps) and on the filter's edge, where the other part
+// matters too: their import takes the columns as they are (exact for real fields' spectra).
+template <bool HERM>
 __global__ void full_to_half_kernel(const double2* __restrict__ full, double2* __restrict__ hs,
                                     int nx, int ny) {
   const size_t n = (size_t)(nx / 2 + 1) * ny;
@@ -451,8 +531,12 @@ __global__ void full_to_half_kernel(const double2* __restrict__ full, double2* _
        t += (size_t)gridDim.x * blockDim.x) {
     const int m = (int)(t / ny), k = (int)(t % ny);
     const double2 a = full[(size_t)k * nx + m];
-    const double2 b = full[(size_t)(k == 0 ? 0 : ny - k) * nx + (m == 0 ? 0 : nx - m)];
-    hs[t] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+    if constexpr (HERM) {
+      const double2 b = full[(size_t)(k == 0 ? 0 : ny - k) * nx + (m == 0 ? 0 : nx - m)];
+      hs[t] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
+    } else {
+      hs[t] = a;
+    }
   }
 }
 // The same projection on the full layout: out(k) = (full(k) + conj(full(-k))) / 2.
@@ -527,6 +611,12 @@ struct cfdj_spec {
   // ones; any even grid); CFDJ_SPEC_REAL=0 or CFDJ_SPEC_FFT=rocfft keep the complex plans
   bool real32 = false;
   rocfft_plan inv_r = nullptr, fwd_r = nullptr;  // Z2D batch 4, D2Z on px x py
+  // ... or, on product grids of 1536 / 3072 / 6144 points a side, the hand-written
+  // 3 * 2^k transforms on the columns 0..nx/2 of that half spectrum (fft2d_r2c3.hip;
+  // CFDJ_SPEC_PS32_HAND=0 keeps the library)
+  bool hand32 = false;
+  Real2d3Args a3{};
+  double2 *tw3_l3 = nullptr, *tw3_l = nullptr, *tw3_n = nullptr, *tw3_m3 = nullptr;
   Fused fz;
   HalfSpecArgs ha{};
   size_t nh() const { return (size_t)(nx / 2 + 1) * ny; }
@@ -597,6 +687,20 @@ struct cfdj_spec {
       return;
     }
     const bool r32 = kind == CFDJ_SPEC_PS32;
+    if (hand32) {
+      const double sc = (double)px * py, sd = (double)nx * ny;
+      hipLaunchKernelGGL(ps32_derivs_cols_kernel, dim3((nx / 2 + 1 + 15) / 16, py / 16), dim3(256),
+                         0, stream, wf, kx, X, nx, ny, px, py, sc, sd);
+      CFDJ_HIP(hipGetLastError());
+      launch_c2r2d3(a3, X, R, 4, stream);
+      product_real(gb, 1.0 / sc);
+      CFDJ_HIP(hipGetLastError());
+      launch_r2c2d3(a3, Rj, J, stream);
+      hipLaunchKernelGGL(ps32_unpad_cols_kernel, dim3(nx / 16, ny / 16), dim3(256), 0, stream, J,
+                         jf, nx, ny, px, py, sd, sc);
+      CFDJ_HIP(hipGetLastError());
+      return;
+    }
     if (real32) {
       const double sc = (double)px * py, sd = (double)nx * ny;
       const size_t nhp = (size_t)(px / 2 + 1) * py;
@@ -661,19 +765,21 @@ struct cfdj_spec {
   // Full spectrum in `full` (device) -> the state layout in `dst`, and back.
   void import_spectrum(const double2* full, double2* dst) {
     if (half) {
-      hipLaunchKernelGGL(full_to_half_kernel, dim3(grid_for(nh())), dim3(256), 0, stream, full,
-                         dst, nx, ny);
+      if (kind == CFDJ_SPEC_HYBRID)
+        hipLaunchKernelGGL(full_to_half_kernel<true>, dim3(grid_for(nh())), dim3(256), 0, stream,
+                           full, dst, nx, ny);
+      else
+        hipLaunchKernelGGL(full_to_half_kernel<false>, dim3(grid_for(nh())), dim3(256), 0, stream,
+                           full, dst, nx, ny);
       CFDJ_HIP(hipGetLastError());
-    } else if (kind != CFDJ_SPEC_PS32) {
-      // hybrid.jl:103,115 and pseudospectral_23_rule.jl:135-138 see w_f through real(ifft(.))
-      // of spectra whose multipliers are Hermitian (the 2/3 rule zeroes the Nyquist modes),
-      // i.e. its Hermitian part only; the real-field transforms here assume that symmetry
+    } else if (kind == CFDJ_SPEC_HYBRID) {
+      // hybrid.jl:103,115 sees w_f through real(ifft(.)) of w_f and w_f / k2 (k2 even), i.e.
+      // its Hermitian part only; the real-field transforms here assume that symmetry
       hipLaunchKernelGGL(hermitian_part_kernel, dim3(grid_for(n())), dim3(256), 0, stream, full,
                          dst, nx, ny);
       CFDJ_HIP(hipGetLastError());
     } else {
-      // 3/2 rule: the padded Nyquist modes enter with their own value (no mirror partner in
-      // the padded spectrum, pseudospectral_32_rule.jl:124-133): kept as given
+      // pseudospectral rules: kept as given (see full_to_half_kernel)
       CFDJ_HIP(hipMemcpyAsync(dst, full, n() * sizeof(double2), hipMemcpyDeviceToDevice, stream));
     }
   }
@@ -705,6 +811,7 @@ struct cfdj_spec {
     plans.destroy();
     if (tw_p != tw_n) dfree(tw_p);
     dfree(tw_n);
+    for (double2** p : {&tw3_l3, &tw3_l, &tw3_n, &tw3_m3}) dfree(*p);
     for (double2** p : {&wn, &w1, &w2, &jn, &j1, &j2, &X, &J}) dfree(*p);
     dfree(R);
     dfree(Rj);
@@ -778,6 +885,17 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
                            ny - nye / 2, h->stream_loads};
     }
     h->real32 = kind == CFDJ_SPEC_PS32 && want_hand && want_real;
+    const char* h32 = std::getenv("CFDJ_SPEC_PS32_HAND");
+    h->hand32 = h->real32 && real2d3_supported(h->px) && nx % 16 == 0 &&
+                !(h32 && h32[0] == '0');
+    if (h->hand32) {
+      h->tw3_l3 = twiddle_table(h->px / 6);
+      h->tw3_l = twiddle_table(h->px / 2);
+      h->tw3_n = twiddle_table(h->px);
+      h->tw3_m3 = twiddle_table(h->px / 3);
+      h->a3 = Real2d3Args{h->px, nx / 2, h->tw3_l3, h->tw3_l, h->tw3_n, h->tw3_m3,
+                          h->stream_loads};
+    }
     if (h->real_fields || h->half || h->real32) {
       h->R = dalloc<double>((size_t)nb * np);
       h->Rj = dalloc<double>(np);
@@ -801,7 +919,7 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     if (kind == CFDJ_SPEC_PS32 && !h->real32)
       h->fwd_p = h->plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace,
                               2, lp, 1, nullptr);
-    if (h->real32) {
+    if (h->real32 && !h->hand32) {
       h->inv_r = h->plans.add(rocfft_transform_type_real_inverse, rocfft_placement_notinplace,
                               2, lp, nb, nullptr);
       h->fwd_r = h->plans.add(rocfft_transform_type_real_forward, rocfft_placement_notinplace,

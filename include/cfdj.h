@@ -269,11 +269,13 @@ int cfdj_spec_step(cfdj_spec* h, double dt, int nsteps);
 /* hybrid.jl:71-76: ut = real(ifft(w_f)) on (nx+1) x (ny+1) nodes (ld >= nx+1). */
 int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu);
 /* w_f itself, complex nx x ny column-major as interleaved (re, im) doubles.  w_f is the
- * spectrum of a real field (the only kind the reference's loop produces): where the solver
- * keeps half of it (square power-of-two grids of 1024..8192, hybrid and 2/3 rule),
+ * spectrum of a real field (the only kind the reference's loop produces).  The hybrid solver's
  * set_spectrum and jacobian keep the Hermitian part (w_f(k) + conj(w_f(-k))) / 2 of their
- * input -- all that the reference's jacobian() sees through real(ifft(.)), so cfdj_spec_jacobian
- * matches it for any input -- and get_spectrum returns that part with its conjugate mirror. */
+ * input -- all that hybrid.jl's jacobian() sees of it through real(ifft(.)), so
+ * cfdj_spec_jacobian matches it for any input.  The pseudospectral rules require the spectrum
+ * of a real field: where the solver keeps half of it (square power-of-two grids of
+ * 1024..8192, 2/3 rule) they read the modes kx index 0..nx/2 and take the others to be their
+ * conjugate mirror.  get_spectrum returns the state with its conjugate mirror. */
 int cfdj_spec_get_spectrum(cfdj_spec* h, double* wf);
 int cfdj_spec_set_spectrum(cfdj_spec* h, const double* wf);
 /* One `jacobian(nx, ny, dx, dy, wf, k2)` call: jf = fft(-J(w, psi)) (complex, as above). */

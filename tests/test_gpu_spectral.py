@@ -196,10 +196,11 @@ def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
 
 @pytest.mark.parametrize("kind", ["hybrid", "2/3"])
 def test_gpu_spectral_half_spectrum_round_trip(spec, kind):
-    """set_spectrum / spectrum through the half-spectrum state (n = 1024): the Hermitian part
-    (w_f(k) + conj(w_f(-k))) / 2 of what went in comes back bit for bit, its Nyquist row and
-    column included -- for the spectrum of a real field that is the spectrum itself, up to
-    the last-bit asymmetries of the CPU FFT that produced it."""
+    """set_spectrum / spectrum through the half-spectrum state (n = 1024), Nyquist row and
+    column included, bit for bit: the hybrid solver returns the Hermitian part (w_f(k) +
+    conj(w_f(-k))) / 2 of what went in -- for the spectrum of a real field the spectrum itself,
+    up to the last-bit asymmetries of the CPU FFT that produced it -- the 2/3 rule the kx
+    columns 0..n/2 as given and their conjugate mirror."""
     n = 1024
     dx, dy, _, _ = vo.vm_grid(n, n)
     f = smooth_field(n, n, 5, n) + 0.01 * np.random.default_rng(7).standard_normal((n, n))
@@ -208,7 +209,7 @@ def test_gpu_spectral_half_spectrum_round_trip(spec, kind):
         h.set_spectrum(wf)
         back = h.spectrum()
     mirror = np.conj(wf[(-np.arange(n)) % n][:, (-np.arange(n)) % n])
-    herm = 0.5 * (wf + mirror)
+    herm = 0.5 * (wf + mirror) if kind == "hybrid" else wf
     assert np.abs(herm - wf).max() <= 1e-15 * np.abs(wf).max()
     i = np.arange(n // 2 + 1)
     assert np.array_equal(back[i, :], herm[i, :])
@@ -251,19 +252,44 @@ def test_gpu_spectral_argument_errors(spec):
         spec.SpectralNS2D(63, 63, dx, dx, 1000.0)  # odd nx
 
 
-@pytest.mark.parametrize("kind", KINDS)
-def test_gpu_spectral_jacobian_of_a_non_hermitian_spectrum(spec, kind):
-    """hybrid.jl:92-152 / pseudospectral_23_rule.jl:95-144 take real(ifft(.)) of what they are
-    given, i.e. they see the Hermitian part of w_f only (the 3/2 rule's padded Nyquist modes
-    apart, pseudospectral_32_rule.jl:124-133).  A w_f that is NOT the spectrum of a real field
-    must therefore give the oracle's Jacobian on the half-spectrum path (n = 1024) as on the
-    full-spectrum ones (n = 96: library transforms, n = 256: hand-written)."""
+def test_gpu_spectral_jacobian_of_a_non_hermitian_spectrum(spec):
+    """hybrid.jl:92-152 takes real(ifft(.)) of w_f and of w_f / k2 (k2 even), i.e. it sees the
+    Hermitian part of w_f only.  A w_f that is NOT the spectrum of a real field must therefore
+    give the oracle's Jacobian on the half-spectrum path (n = 1024) as on the full-spectrum
+    ones (n = 96: library transforms, n = 256: hand-written).  (The pseudospectral rules'
+    i k and band-filter multipliers are not Hermitian at index 1 and on the filter's edge:
+    they are defined here for spectra of real fields, like the reference's loop produces.)"""
     for n in (96, 256, 1024):
         dx, dy, _, _ = vo.vm_grid(n, n)
         rng = np.random.default_rng(7 * n)
         wf = _noisy_spectrum(n) + n * (rng.standard_normal((n, n))
                                        + 1j * rng.standard_normal((n, n)))
-        ref = so.JACOBIANS[KIND_ID[kind]](wf, so.wavespace(n, n, dx, dy), dx, dy)
-        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
+        wf[0, 0] = 0.0  # as every spectrum of the loop (hybrid.jl:28): k2[1,1] = 2 eps^2
+        ref = so.jacobian_hybrid(wf, so.wavespace(n, n, dx, dy), dx, dy)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, "hybrid") as h:
             got = h.jacobian(wf)
         assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), n
+
+
+@pytest.mark.parametrize("n", [1024, 4096])
+def test_gpu_spectral_32_rule_hand_transforms_vs_library(spec, monkeypatch, n):
+    """pseudospectral_32_rule.jl:94-186 on product grids of 3 * 2^k points (1536, 6144 = 1.5 x
+    the benchmarked 4096): the hand-written radix-3 + power-of-two transforms on the columns
+    0..nx/2 of the padded half spectrum (fft2d_r2c3.hip) against the library's real transforms
+    (CFDJ_SPEC_PS32_HAND=0) on a field with content in every mode: one Jacobian to 1e-12 of
+    max|jf|, and at 1024 also against the oracle."""
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    wf = _noisy_spectrum(n)
+    out = {}
+    for name, env in (("hand", None), ("library", "0")):
+        monkeypatch.delenv("CFDJ_SPEC_PS32_HAND", raising=False)
+        if env is not None:
+            monkeypatch.setenv("CFDJ_SPEC_PS32_HAND", env)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, "3/2") as h:
+            out[name] = h.jacobian(wf)
+    scale = np.abs(out["library"]).max()
+    assert np.isfinite(out["hand"]).all()
+    assert np.abs(out["hand"] - out["library"]).max() <= 1e-12 * scale
+    if n == 1024:
+        ref = so.jacobian_ps32(wf, so.wavespace(n, n, dx, dy), dx, dy)
+        assert np.abs(out["hand"] - ref).max() <= 1e-12 * np.abs(ref).max()
