@@ -323,6 +323,68 @@ __global__ __launch_bounds__(DstNpCfg<M2>::THREADS) void dst_rows_inv_np_kernel(
   }
 }
 
+// The forward row pass in the same small-item shape (CFDJ_DST_FWD_NP): the packed transform's
+// outputs go through the buffer one component at a time into natural order; an entry of the
+// pair's first row needs the imaginary parts only (-Im Z), one of its second row the real
+// parts (Re Z).
+#ifndef CFDJ_DST_FWD_NP
+#define CFDJ_DST_FWD_NP 1
+#endif
+template <int M2>
+constexpr bool dst_fwd_np() { return CFDJ_DST_FWD_NP != 0 && M2 <= 4096; }
+
+template <int M2>
+__global__ __launch_bounds__(DstNpCfg<M2>::THREADS) void dst_rows_fwd_np_kernel(
+    const double* __restrict__ w, int P, int ny, double2* __restrict__ T, int JT, double sgn,
+    const double2* __restrict__ tw_) {
+  using PL = Plan<M2>;
+  using C = DstNpCfg<M2>;
+  __shared__ double lds[C::RP * PL::PAD];
+  const TwGlobal<M2> tw{tw_};
+  const int q = threadIdx.x / PL::T, tid = threadIdx.x % PL::T;
+  double* buf = lds + q * PL::PAD;
+  const int slot0 = xcd_remap(blockIdx.x, gridDim.x) * C::ROWS;
+  double2 v[16];
+  load_row_pair<M2>(v, w, P, ny, 1 + slot0 + 2 * q, tid, sgn);
+  stage_regs<M2, 0, -1>(v, tid, tw);
+  run_stages_half<M2, 1, -1>(buf, v, tid, tw);
+  constexpr int SL = PL::NSTAGES - 1;
+  constexpr int RL = PL::radix(SL);
+  auto entry = [](int i, int& rr, int& kap) {
+    const int e = threadIdx.x + i * C::THREADS;
+    rr = (e >> 4) % C::ROWS;
+    kap = ((e >> 4) / C::ROWS) * 16 + (e & 15);
+  };
+  double2 o[C::ENTRIES];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();
+#pragma unroll
+    for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+      for (int r = 0; r < RL; ++r)
+        buf[padx(out_pos<M2, SL>(tid, b, r))] = c ? v[b * RL + r].y : v[b * RL + r].x;
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < C::ENTRIES; ++i) {
+      int rr, kap;
+      entry(i, rr, kap);
+      if ((rr & 1) != c) {  // second row of a pair: Re Z (c = 0); first row: -Im Z (c = 1)
+        const double* bq = lds + (rr >> 1) * PL::PAD;
+        const double z0 = bq[padx(2 * kap)], z1 = bq[padx(2 * kap + 1)];
+        o[i] = c ? make_double2(-z0, -z1) : make_double2(z0, z1);
+      }
+    }
+  }
+  double2* tb = T + __builtin_amdgcn_readfirstlane(slot0);
+#pragma unroll
+  for (int i = 0; i < C::ENTRIES; ++i) {
+    int rr, kap;
+    entry(i, rr, kap);
+    tb[(unsigned)(kap * JT + rr)] = o[i];
+  }
+}
+
 // One mode pair per workgroup: packed y-DST, times iden, packed y-DST, in place.
 #ifndef CFDJ_DST_COLS_WAVES
 #define CFDJ_DST_COLS_WAVES 3
@@ -418,7 +480,11 @@ template <int M2>
 void launch_dst_rows(int pass, const DstPoissonArgs& a, hipStream_t st) {
   using C = DstRowCfg<M2>;
   const dim3 grid(dst_rows_grid_t<M2>(a.ny, a.ncu));
-  if (pass == 0) {
+  if (pass == 0 && dst_fwd_np<M2>() && a.ny % DstNpCfg<M2>::ROWS == 0) {
+    hipLaunchKernelGGL((dst_rows_fwd_np_kernel<M2>), dim3(a.ny / DstNpCfg<M2>::ROWS),
+                       dim3(DstNpCfg<M2>::THREADS), 0, st, a.w, a.P, a.ny, a.T, a.JT,
+                       a.neg ? -1.0 : 1.0, a.twX);
+  } else if (pass == 0) {
     hipLaunchKernelGGL((dst_rows_fwd_kernel<M2>), grid, dim3(C::THREADS), 0, st, a.w, a.P, a.ny,
                        a.T, a.JT, a.neg ? -1.0 : 1.0, a.twX);
   } else if (dst_inv_np<M2>() && a.ny % DstNpCfg<M2>::ROWS == 0) {
