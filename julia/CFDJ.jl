@@ -8,6 +8,7 @@
 #   lid_driven_cavity.jl:197  CFDJ.cavity_numerical(nx, ny, nt, Δx, Δy, Δt, re, wn, sn, rms)
 #   lid_driven_cavity.jl:84   CFDJ.fps_sine(nx, ny, Δx, Δy, f, u, e, data, data1, iden, sn)
 #   lid_driven_cavity.jl:78   CFDJ.cavity_rhs(nx, ny, Δx, Δy, re, w, s, r)
+#   fft_d.jl:73      un[2:nx, 2:ny] = CFDJ.ps_fst(nx, ny, Δx, Δy, f)
 #   mg_N.jl:180      CFDJ.mg_N(Δx, Δy, nx, ny, r, f, u_n, v1, v2, v3, max_iter, tol, out, n_level)
 #   mg.jl:146        CFDJ.mg(Δx, Δy, nx, ny, r, f, u_n, v1, v2, v3, max_iter, tol, out)
 #
@@ -190,6 +191,15 @@ function fps_sine(nx, ny, Δx, Δy, f, u, e, data, data1, iden, sn)
                 (Cint, Cint, Cdouble, Cdouble, Ptr{Cdouble}, Clong, Ptr{Cdouble}, Clong),
                 nx, ny, Δx, Δy, f, size(f, 1), sn, size(sn, 1)), "cfdj_fps_sine")
     return nothing
+end
+
+"14_Poisson_Solver_FST/fft_d.jl:7-23: the (nx-1) x (ny-1) interior solution for f[2:nx, 2:ny]."
+function ps_fst(nx, ny, Δx, Δy, f)
+    sn = zeros(Float64, nx + 1, ny + 1)
+    check(ccall((:cfdj_fps_sine, libcfdj), Cint,
+                (Cint, Cint, Cdouble, Cdouble, Ptr{Cdouble}, Clong, Ptr{Cdouble}, Clong),
+                nx, ny, Δx, Δy, f, size(f, 1), sn, size(sn, 1)), "cfdj_fps_sine")
+    return sn[2:nx, 2:ny]
 end
 
 # ---- 17_Poisson_Solver_Multigrid/mg_N.jl and mg.jl ------------------------------------------
