@@ -27,6 +27,29 @@ namespace cfdj {
 
 namespace {
 
+// exp(-2 pi i j / 48), j < 16: the radix-3 step's twiddle of output k = tid + T3 j is that of
+// k = tid times this constant (T3 / L = 1/48); exp(-2 pi i j / 32), j < 8: the same for the
+// real-transform post-processing's W_N^m, m = m0 + TT j (TT / N = 1/32).  One table load per
+// thread instead of one per output.
+__device__ constexpr double kC48[16] = {
+    1.0, 0.99144486137381038, 0.96592582628906831, 0.92387953251128674,
+    0.86602540378443871, 0.79335334029123517, 0.70710678118654757, 0.60876142900872066,
+    0.5, 0.38268343236508984, 0.25881904510252074, 0.13052619222005171,
+    0.0, -0.1305261922200516, -0.25881904510252063, -0.3826834323650895};
+__device__ constexpr double kS48[16] = {
+    0.0, 0.13052619222005157, 0.25881904510252074, 0.38268343236508978,
+    0.5, 0.60876142900872066, 0.70710678118654746, 0.79335334029123517,
+    0.8660254037844386, 0.92387953251128674, 0.96592582628906831, 0.99144486137381038,
+    1.0, 0.99144486137381038, 0.96592582628906831, 0.92387953251128685};
+__device__ constexpr double kC32[8] = {1.0, 0.98078528040323043, 0.92387953251128674,
+                                       0.83146961230254524, 0.70710678118654757,
+                                       0.55557023301960229, 0.38268343236508984,
+                                       0.19509032201612833};
+__device__ constexpr double kS32[8] = {0.0, 0.19509032201612825, 0.38268343236508978,
+                                       0.55557023301960218, 0.70710678118654746,
+                                       0.83146961230254524, 0.92387953251128674,
+                                       0.98078528040323043};
+
 template <int L3>
 struct Cfg3 {
   static constexpr int L = 3 * L3;
@@ -73,12 +96,12 @@ __device__ __forceinline__ void combine3(double* team_buf, const double2 (&v)[16
     // second pass instead of staying live (64 registers) across the exchange
     int tk = tid;
     asm volatile("" : "+v"(tk));
+    double2 cb = twL[tk + q * L3];  // W_L^p of the thread's first output
+    if (DIR > 0) cb.y = -cb.y;
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int k = tk + C::T3 * j;
-      const int p = k + q * L3;
-      double2 c1 = twL[p];
-      if (DIR > 0) c1.y = -c1.y;
+      const double2 c1 = cmul(cb, make_double2(kC48[j], DIR < 0 ? -kS48[j] : kS48[j]));
       const double2 c2 = cmul(c1, c1);
       const double f0 = team_buf[padx(k)], f1 = team_buf[padx(L3 + k)],
                    f2 = team_buf[padx(2 * L3 + k)];
@@ -157,7 +180,9 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
   const double2* base = H + __builtin_amdgcn_readfirstlane(y0);
   // c2r pre-processing of the pairs (m, L - m): Z[m] = (X[m] + conj X[L-m]) + i W_N^-m (X[m] -
   // conj X[L-m]); slot 0 = X[0] (the Nyquist mode of this grid is zero), Z[L/2] = 2 conj X[L/2]
+  static_assert(PAIRS == 8, "pair twiddle table");
   double2 o1[PAIRS], o2[PAIRS];
+  double2 wn0 = make_double2(1.0, 0.0);
 #pragma unroll
   for (int i = 0; i < PAIRS; ++i) {
     int qq, m;
@@ -169,7 +194,8 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
     if (mq <= mmax) Xq = base[(size_t)mq * M + qq];
     const double2 Xp = cconj(Xq);
     const double2 S = cadd(Xm, Xp);
-    const double2 D = cmul(cconj(twN[m]), csub(Xm, Xp));
+    if (i == 0) wn0 = cconj(twN[m]);  // W_N^-m of pair 0; pair i: m + TT i
+    const double2 D = cmul(cmul(wn0, make_double2(kC32[i], kS32[i])), csub(Xm, Xp));
     o1[i] = make_double2(S.x - D.y, S.y + D.x);
     o2[i] = make_double2(S.x + D.y, D.x - S.y);
     if (z0) {
@@ -252,6 +278,8 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
     }
   }
   double2* hb = H + __builtin_amdgcn_readfirstlane(y0);
+  static_assert(PAIRS == 8, "pair twiddle table");
+  double2 wn0 = make_double2(1.0, 0.0);
 #pragma unroll
   for (int i = 0; i < PAIRS; ++i) {
     int qq, m;
@@ -262,7 +290,8 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
     const double2 E = make_double2(0.5 * (Zm[i].x + Zc.x), 0.5 * (Zm[i].y + Zc.y));
     const double2 D = csub(Zm[i], Zc);
     const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);
-    const double2 WO = cmul(twN[m], O);
+    if (i == 0) wn0 = twN[m];  // W_N^m of pair 0; pair i: m + TT i
+    const double2 WO = cmul(cmul(wn0, make_double2(kC32[i], -kS32[i])), O);
     double2 o1 = cadd(E, WO);
     double2 o2 = cconj(csub(E, WO));
     if (z0) {  // slot 0 = X[0] (this grid's Nyquist mode X[L] is not kept); X[L/2] = conj Z[L/2]
