@@ -320,6 +320,23 @@ bool real2d3_supported(int n);
 void launch_c2r2d3(const Real2d3Args& a, double2* x, double* r, int batch, hipStream_t st);
 // x = columns 0..mmax of fft2(r).
 void launch_r2c2d3(const Real2d3Args& a, const double* r, double2* x, hipStream_t st);
+// The same transforms for the 3/2-rule solver on the half spectrum hs of its UNPADDED grid
+// (columns m = 0..N/2 of N = 2n/3 elements, ky contiguous, then the N/2 + 1 elements
+// w_f(-m, N/2), m = 0..N/2, which that solver's spectra do not share with their other half;
+// a.mmax = N/2): the padding and the derivative factors of pseudospectral_32_rule.jl:109-154
+// are applied where the inverse column pass loads a column, the unpadding of :171-178 where the
+// forward one stores it.
+struct Ps32HalfArgs {
+  const double* kx;   // the reference's wavenumber table of the unpadded grid (kx[0] = eps)
+  double scale_in;    // (nxe nye) / (nx ny)
+  double scale_out;   // (nx ny) / (nxe nye)
+};
+// r[b] = real(ifft2(padded derivative spectrum b of hs)), b < 4; x: 4 x (mmax + 1) x n scratch.
+void launch_ps32_c2r2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double2* hs, double2* x,
+                        double* r, hipStream_t st);
+// hs = unpadded fft2(r) (columns 0..N/2); x: (mmax + 1) x n scratch.
+void launch_ps32_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double* r, double2* x,
+                        double2* hs, hipStream_t st);
 
 // Substructured y-solve of the y-slab Poisson path (schur.hip): per x-mode
 // m = 1..L-1, the periodic y-tridiagonal of the reference symbol split at one separator row

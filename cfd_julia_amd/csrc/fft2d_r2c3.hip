@@ -146,6 +146,133 @@ __global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_kernel(
   for (int j = 0; j < 16; ++j) col[tid + C::T3 * j + q * M3] = o[j];
 }
 
+// ---- columns of the 3/2-rule solver on the half spectrum of its unpadded grid ---------------
+// State layout: columns m = 0..N/2 of N = 2 M3 elements (ky contiguous), the modes kx index
+// 0..N/2 of the spectrum, followed by the row `ex` of N/2 + 1 elements ex[m] = w_f(-m, N/2).
+// The rest of the other half is conj(w_f(-kx, -ky)), as for any real field's spectrum; the ky
+// index N/2 is different: the 3/2 rule's unpadding (pseudospectral_32_rule.jl:171-178) fills it
+// with the padded grid's mode -N/2, which on that grid is not its own conjugate twin, so
+// w_f(-m, N/2) and conj(w_f(m, N/2)) are independent numbers from the first Jacobian on, and
+// so are w_f(N/2, j) and conj(w_f(N/2, -j)) -- column N/2 is stored whole anyway.
+// The padded column has 3 M3 elements, the unpadded modes in its first and last third
+// (pseudospectral_32_rule.jl:109-154).
+
+// Inverse column pass with the four derivative spectra formed where the column is loaded:
+// array arr of i kx w_f / k2, i ky w_f, i ky w_f / k2, i kx w_f (pseudospectral_32_rule.jl:
+// 109-154), padded, times `scale` = (nxe nye) / (nx ny).  real(ifft(.)) keeps the Hermitian
+// part (P(a, b) + conj P(-a, -b)) / 2 of the padded array P; at the padded element p of column
+// a0 that is (i/2) (kappa(a0, j) w_f(a0, j) - kappa(-a0, -j) conj w_f(-a0, -j)) (/ k2), j the
+// unpadded mode at p, each term present only where the padding puts that mode: the index N/2
+// is the mode -N/2 and sits on the negative side only (so column N/2 and the element 2 M3 have
+// no first term, the element M3 -- the twin of the other side's 2 M3 -- no second), and kappa
+// is not odd at index 0 (kx[1] = eps, Common.jl:199).  EDGE = the columns 0 and N/2, which hold
+// both w_f(a0, j) and w_f(-a0, -j) = w_f(a0, -j); elsewhere the second is the conjugate of the
+// first, except at the element M3, where it is ex[a0].
+template <int M3, bool EDGE>
+__device__ __forceinline__ void ps32_load_column(double2 (&v)[16], const double2* __restrict__ col,
+                                                 double2 ex, const double* __restrict__ kx, int a0,
+                                                 int arr, int q, int tid, double scale) {
+#pragma clang fp contract(off)
+  using C = Cfg3<M3>;
+  constexpr int N = 2 * M3, H = M3;
+  const bool fp = a0 < H;
+  const double kxa = kx[a0], kxm = kx[(N - a0) & (N - 1)];
+  const bool xder = arr == 0 || arr == 3, overk2 = arr == 0 || arr == 2;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int p = 3 * (tid + C::T3 * r) + q;
+    const bool kept = p <= H || p >= 2 * H;
+    const int j = p <= H ? p : p - H;  // (the middle third maps to a valid index, unused)
+    const int jm = (N - j) & (N - 1);
+    const double kyj = kx[j], kym = kx[jm];
+    const double kap_p = fp && p != H ? (xder ? kxa : kyj) : 0.0;
+    const double kap_m = p != 2 * H ? (xder ? kxm : kym) : 0.0;
+    double2 u;  // kappa(a0, j) w_f(a0, j) - kappa(-a0, -j) conj(w_f(-a0, -j))
+    if constexpr (EDGE) {
+      const double2 w0 = col[j], w1 = col[jm];
+      u = make_double2(kap_p * w0.x - kap_m * w1.x, kap_p * w0.y + kap_m * w1.y);
+    } else {
+      double2 w = col[j];
+      if (p == H) w = make_double2(ex.x, -ex.y);
+      const double keff = kap_p - kap_m;
+      u = make_double2(keff * w.x, keff * w.y);
+    }
+    double f = 0.5 * scale;
+    if (overk2) f = f * recip_nr(kxa * kxa + kyj * kyj);
+    v[r] = kept ? make_double2(f * -u.y, f * u.x) : make_double2(0.0, 0.0);  // i u f
+  }
+}
+
+template <int M3>
+__global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_ps32_in_kernel(
+    const double2* __restrict__ hs, double2* __restrict__ x, const double* __restrict__ kx,
+    double scale, const double2* __restrict__ tw3, const double2* __restrict__ twM) {
+  using C = Cfg3<M3>;
+  constexpr int N = 2 * M3;
+  __shared__ double lds[C::PADL];
+  // the four arrays of a column are neighbours (one XCD): the column comes from HBM once
+  const int id = xcd_remap(blockIdx.x, gridDim.x);
+  const int a0 = __builtin_amdgcn_readfirstlane(id >> 2), arr = id & 3;
+  const double2* col = hs + (size_t)a0 * N;
+  const double2 ex = hs[(size_t)(M3 + 1) * N + a0];
+  const int t = threadIdx.x, q = t / C::T3, tid = t % C::T3;
+  double2 v[16];
+  if (a0 == 0 || a0 == M3) ps32_load_column<M3, true>(v, col, ex, kx, a0, arr, q, tid, scale);
+  else ps32_load_column<M3, false>(v, col, ex, kx, a0, arr, q, tid, scale);
+  sub_fft<M3, 1>(lds, v, q, tid, tw3);
+  double2 o[16];
+  combine3<M3, 1>(lds, v, q, tid, twM, o);
+  double2* out = x + ((size_t)arr * (M3 + 1) + a0) * C::L;
+#pragma unroll
+  for (int j = 0; j < 16; ++j) out[tid + C::T3 * j + q * M3] = o[j];
+}
+
+// Forward column pass with the unpadding of pseudospectral_32_rule.jl:171-178 where the column
+// is stored, times `scale` = (nx ny) / (nxe nye): the first third of the padded column a0 is
+// the state's modes 0..N/2-1 of that column, the last third its modes N/2..N-1; the middle
+// third is dropped but for its first element M3, the mode (a0, +N/2), whose conjugate is the
+// state's ex[a0] = (-a0, -N/2).  The state's column N/2 is the mode -N/2: mode j there is the
+// conjugate of the element -b(j) of the padded column N/2, b(j) the padded index of mode j.
+template <int M3>
+__global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_ps32_out_kernel(
+    const double2* __restrict__ x, double2* __restrict__ hs, double scale,
+    const double2* __restrict__ tw3, const double2* __restrict__ twM) {
+  using C = Cfg3<M3>;
+  constexpr int N = 2 * M3, H = M3;
+  __shared__ double lds[C::PADL];
+  const int a0 = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
+  const double2* col = x + (size_t)a0 * C::L;
+  const int t = threadIdx.x, q = t / C::T3, tid = t % C::T3;
+  double2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = col[3 * (tid + C::T3 * r) + q];
+  sub_fft<M3, -1>(lds, v, q, tid, tw3);
+  double2 o[16];
+  combine3<M3, -1>(lds, v, q, tid, twM, o);
+  double2* out = hs + (size_t)a0 * N;
+  double2* ex = hs + (size_t)(M3 + 1) * N;
+  if (a0 != H) {
+    if (q != 1) {
+      double2* ob = out + tid + (q == 2 ? M3 : 0);
+#pragma unroll
+      for (int j = 0; j < 16; ++j) ob[C::T3 * j] = make_double2(o[j].x * scale, o[j].y * scale);
+    } else if (tid == 0) {
+      ex[a0] = make_double2(o[0].x * scale, -o[0].y * scale);
+    }
+  } else {
+    // element p goes to j = -p of the first and the last third; the padding puts -b = N/2 in
+    // the last third's twin only: element M3 -> j = N/2 (and ex[N/2], the same mode)
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int p = tid + C::T3 * j + q * M3;
+      const double2 c = make_double2(o[j].x * scale, -o[j].y * scale);
+      if (q == 0) out[(N - p) & (N - 1)] = c;
+      else if (q == 2 && p != 2 * M3) out[C::L - p] = c;
+      else if (q == 1 && p == M3) out[H] = ex[H] = c;
+    }
+  }
+}
+
 // Pair i of a thread in a row workgroup of XR teams: row qq, columns m and L - m; 16
 // consecutive lanes take 16 consecutive m of one row (whole XR * 16-B column segments).
 template <int L3, int XR>
@@ -345,6 +472,18 @@ void launch_cols3(bool fwd, const Real2d3Args& a, double2* x, int batch, hipStre
   else hipLaunchKernelGGL((cols3_kernel<M3, 1>), grid, block, 0, st, x, a.tw3M, a.twN);
 }
 
+template <int M3>
+void launch_cols3_ps32(bool fwd, const Real2d3Args& a, const Ps32HalfArgs& s, const double2* src,
+                       double2* dst, hipStream_t st) {
+  const dim3 block(Cfg3<M3>::TT);
+  if (fwd)
+    hipLaunchKernelGGL((cols3_ps32_out_kernel<M3>), dim3((unsigned)(M3 + 1)), block, 0, st, src,
+                       dst, s.scale_out, a.tw3M, a.twN);
+  else
+    hipLaunchKernelGGL((cols3_ps32_in_kernel<M3>), dim3((unsigned)(4 * (M3 + 1))), block, 0, st,
+                       src, dst, s.kx, s.scale_in, a.tw3M, a.twN);
+}
+
 void check3(const Real2d3Args& a) {
   if (!real2d3_supported(a.n) || a.mmax < 0 || a.mmax >= a.n / 2 || a.n % CFDJ_ROWS3_XR != 0 ||
       a.n % CFDJ_ROWS3_FWD_XR != 0)
@@ -388,6 +527,52 @@ void launch_r2c2d3(const Real2d3Args& a, const double* r, double2* x, hipStream_
     default:
       launch_rows3<1024>(true, a, r, nullptr, x, st);
       launch_cols3<2048>(true, a, x, 1, st);
+      break;
+  }
+  CFDJ_HIP(hipGetLastError());
+}
+
+// The 3/2-rule solver's transforms between its half-spectrum state and the padded grid.
+static void check_ps32(const Real2d3Args& a) {
+  check3(a);
+  if (a.mmax != a.n / 3) throw Error{CFDJ_ERR_ARG, "3/2-rule transform: mmax must be n / 3"};
+}
+
+void launch_ps32_c2r2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double2* hs, double2* x,
+                        double* r, hipStream_t st) {
+  check_ps32(a);
+  const size_t half = (size_t)(a.mmax + 1) * a.n, full = (size_t)a.n * a.n;
+  switch (a.n) {
+    case 1536: launch_cols3_ps32<512>(false, a, s, hs, x, st); break;
+    case 3072: launch_cols3_ps32<1024>(false, a, s, hs, x, st); break;
+    default: launch_cols3_ps32<2048>(false, a, s, hs, x, st); break;
+  }
+  CFDJ_HIP(hipGetLastError());
+  for (int b = 0; b < 4; ++b) {
+    switch (a.n) {
+      case 1536: launch_rows3<256>(false, a, nullptr, r + b * full, x + b * half, st); break;
+      case 3072: launch_rows3<512>(false, a, nullptr, r + b * full, x + b * half, st); break;
+      default: launch_rows3<1024>(false, a, nullptr, r + b * full, x + b * half, st); break;
+    }
+    CFDJ_HIP(hipGetLastError());
+  }
+}
+
+void launch_ps32_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double* r, double2* x,
+                        double2* hs, hipStream_t st) {
+  check_ps32(a);
+  switch (a.n) {
+    case 1536:
+      launch_rows3<256>(true, a, r, nullptr, x, st);
+      launch_cols3_ps32<512>(true, a, s, x, hs, st);
+      break;
+    case 3072:
+      launch_rows3<512>(true, a, r, nullptr, x, st);
+      launch_cols3_ps32<1024>(true, a, s, x, hs, st);
+      break;
+    default:
+      launch_rows3<1024>(true, a, r, nullptr, x, st);
+      launch_cols3_ps32<2048>(true, a, s, x, hs, st);
       break;
   }
   CFDJ_HIP(hipGetLastError());

@@ -141,7 +141,11 @@ struct Plan {
   static constexpr int ROWSTRIDE = PAD;  // rows kernels: row stride (= 0 mod 64 banks)
 };
 
+#ifdef CFDJ_LDS_XOR
+__device__ __forceinline__ int padx(int i) { return i ^ ((i >> 4) & 15); }
+#else
 __device__ __forceinline__ int padx(int i) { return i + (i >> 4); }
+#endif
 
 // The FD symbol aa + bb cos kx + cc cos ky, evaluated exactly as Common.jl:120 writes it
 // (no FMA): for kx = eps the sum cancels to O(1) from terms of O(nx^2), so a contracted

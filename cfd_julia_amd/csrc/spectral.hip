@@ -462,16 +462,22 @@ __global__ void ps32_unpad_half_kernel(const double2* __restrict__ Jh, double2* 
 // hybrid.jl:44-67, one RK3 / Crank-Nicolson substep.  z = .5dt k2 / re, d = alpha z;
 // out = ((1 - d)/(1 + d)) * w + (cA * jA + cB * jB) / (1 + d)   (stage 1: cB = 0, no jB);
 // out[1,1] = 0 after stages 1 and 2.
-// HALF: the arrays are half spectra ((nx/2 + 1) columns of ny, ky contiguous).
+// HALF: the arrays are half spectra ((nx/2 + 1) columns of ny, ky contiguous), followed by
+// `extra` elements of the modes (-m, ny/2), m = 0..extra-1 (the 3/2 rule's state; k2 is even).
 template <int STAGE, bool HALF, bool NT>
 __global__ void cn_update_kernel(const double2* __restrict__ w, const double2* __restrict__ jA,
                                  const double2* __restrict__ jB, double2* __restrict__ out,
                                  const double* __restrict__ kx, int nx, int ny, double hdt,
-                                 double re, double alpha, double cA, double cB) {
-  const size_t n = HALF ? (size_t)(nx / 2 + 1) * ny : (size_t)nx * ny;
+                                 double re, double alpha, double cA, double cB, int extra) {
+  const size_t nh = (size_t)(nx / 2 + 1) * ny;
+  const size_t n = HALF ? nh + extra : (size_t)nx * ny;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
        t += (size_t)gridDim.x * blockDim.x) {
-    const int i = HALF ? (int)(t / ny) : (int)(t % nx), j = HALF ? (int)(t % ny) : (int)(t / nx);
+    int i = HALF ? (int)(t / ny) : (int)(t % nx), j = HALF ? (int)(t % ny) : (int)(t / nx);
+    if (HALF && t >= nh) {
+      i = (int)(t - nh);
+      j = ny / 2;
+    }
     const double k2 = kx[i] * kx[i] + kx[j] * kx[j];
     const double z = hdt * k2 / re;
     const double d = alpha * z;
@@ -523,12 +529,19 @@ __global__ void to_field_real_kernel(const double* __restrict__ R, double* __res
 // reference's Jacobian.  The pseudospectral rules multiply by i k and a band filter that are
 // not Hermitian at index 1 (kx[1] = eps) and on the filter's edge, where the other part
 // matters too: their import takes the columns as they are (exact for real fields' spectra).
+// `extra` (the 3/2 rule's state): the half spectrum is followed by the row w_f(-m, ny/2),
+// m = 0..nx/2, which that solver's spectra do not share with their other half.
 template <bool HERM>
 __global__ void full_to_half_kernel(const double2* __restrict__ full, double2* __restrict__ hs,
-                                    int nx, int ny) {
+                                    int nx, int ny, int extra) {
   const size_t n = (size_t)(nx / 2 + 1) * ny;
-  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
+  for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n + extra;
        t += (size_t)gridDim.x * blockDim.x) {
+    if (t >= n) {
+      const int m = (int)(t - n);
+      hs[t] = full[(size_t)(ny / 2) * nx + (m == 0 ? 0 : nx - m)];
+      continue;
+    }
     const int m = (int)(t / ny), k = (int)(t % ny);
     const double2 a = full[(size_t)k * nx + m];
     if constexpr (HERM) {
@@ -552,18 +565,38 @@ __global__ void hermitian_part_kernel(const double2* __restrict__ full,
   }
 }
 __global__ void half_to_full_kernel(const double2* __restrict__ hs, double2* __restrict__ full,
-                                    int nx, int ny) {
+                                    int nx, int ny, int extra) {
   const size_t n = (size_t)nx * ny;
   for (size_t t = blockIdx.x * (size_t)blockDim.x + threadIdx.x; t < n;
        t += (size_t)gridDim.x * blockDim.x) {
     const int i = (int)(t % nx), j = (int)(t / nx);
     if (i <= nx / 2) {
       full[t] = hs[(size_t)i * ny + j];
+    } else if (extra && j == ny / 2) {
+      full[t] = hs[(size_t)(nx / 2 + 1) * ny + (nx - i)];
     } else {
       const double2 v = hs[(size_t)(nx - i) * ny + (j == 0 ? 0 : ny - j)];
       full[t] = make_double2(v.x, -v.y);
     }
   }
+}
+
+// The 3/2 rule's extra row of a REAL field's half spectrum: ex[m] = w_f(-m, ny/2) =
+// conj(w_f(m, ny/2)).
+__global__ void ps32_fill_extra_kernel(double2* __restrict__ hs, int nx, int ny) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m > nx / 2) return;
+  const double2 v = hs[(size_t)m * ny + ny / 2];
+  hs[(size_t)(nx / 2 + 1) * ny + m] = make_double2(v.x, -v.y);
+}
+// ... and what real(ifft(.)) keeps of a state whose row ky index ny/2 is not Hermitian:
+// (w_f(m, ny/2) + conj(w_f(-m, ny/2))) / 2 in place of w_f(m, ny/2), 0 < m < nx/2 (the columns
+// 0 and nx/2 are projected by the transform itself).
+__global__ void ps32_project_row_kernel(double2* __restrict__ hs, int nx, int ny) {
+  const int m = blockIdx.x * blockDim.x + threadIdx.x;
+  if (m <= 0 || m >= nx / 2) return;
+  const double2 a = hs[(size_t)m * ny + ny / 2], b = hs[(size_t)(nx / 2 + 1) * ny + m];
+  hs[(size_t)m * ny + ny / 2] = make_double2(0.5 * (a.x + b.x), 0.5 * (a.y - b.y));
 }
 
 unsigned grid_for(size_t n) {
@@ -602,9 +635,10 @@ struct cfdj_spec {
   // real product (real_fields: CFDJ_SPEC_REAL=0 keeps them complex)
   double *R = nullptr, *Rj = nullptr;
   bool real_fields = false;
-  // half-spectrum state (fft2d_r2c.hip; square power-of-two grids of 1024..8192, hybrid and
-  // 2/3 rule): every spectrum above holds the modes kx index 0..nx/2 only, ky contiguous;
-  // the C interface converts (CFDJ_SPEC_HALF=0 keeps the full spectra)
+  // half-spectrum state (fft2d_r2c.hip; square power-of-two grids of 1024..8192: hybrid and
+  // 2/3 rule, and the 3/2 rule where hand32 below holds): every spectrum above holds the modes
+  // kx index 0..nx/2 only, ky contiguous; the C interface converts (CFDJ_SPEC_HALF=0 keeps the
+  // full spectra)
   bool half = false;
   bool stream_loads = false;  // fields beyond the last-level cache: load_stream
   // 3/2 rule: library REAL transforms on the padded grid (half the work of the complex
@@ -616,10 +650,13 @@ struct cfdj_spec {
   // CFDJ_SPEC_PS32_HAND=0 keeps the library)
   bool hand32 = false;
   Real2d3Args a3{};
+  Ps32HalfArgs s3{};
   double2 *tw3_l3 = nullptr, *tw3_l = nullptr, *tw3_n = nullptr, *tw3_m3 = nullptr;
   Fused fz;
   HalfSpecArgs ha{};
   size_t nh() const { return (size_t)(nx / 2 + 1) * ny; }
+  // the 3/2 rule's half-spectrum state carries the row w_f(-m, ny/2) behind the columns
+  int extra() const { return half && kind == CFDJ_SPEC_PS32 ? nx / 2 + 1 : 0; }
 
   // In-place 2-D transform of `batch` arrays: the library plan `pl` or the hand-written one.
   void fft2(rocfft_plan pl, double2* buf, bool product_grid, int batch, int dir) {
@@ -658,6 +695,13 @@ struct cfdj_spec {
         hipLaunchKernelGGL(hybrid_jac_tile_kernel, dim3((nx / 512) * (ny / 2)), dim3(256), 0,
                            stream, R, R + n(), Rj, nx, ny, 1.0 / ((double)nx * ny),
                            1.0 / (4.0 * dx * dy), 1.0 / 3.0);
+      } else if (kind == CFDJ_SPEC_PS32) {
+        // padding, derivative factors and unpadding inside the column passes of the padded grid
+        launch_ps32_c2r2d3(a3, s3, wf, X, R, stream);
+        product_real(gb, 1.0 / ((double)px * py));
+        CFDJ_HIP(hipGetLastError());
+        launch_ps32_r2c2d3(a3, s3, Rj, J, jf, stream);
+        return;
       } else {
         launch_half_c2r2d(ha, kHalfPs23, wf, X, R, stream);
         product_real(gb, 1.0 / ((double)px * py));
@@ -749,11 +793,11 @@ struct cfdj_spec {
   template <int STAGE>
   void update(const double2* w, const double2* jA, const double2* jB, double2* out, double dt,
               double alpha, double cA, double cB) {
-    const dim3 g(grid_for(half ? nh() : n())), b(256);
+    const dim3 g(grid_for(half ? nh() + extra() : n())), b(256);
     const double hdt = 0.5 * dt;
 #define CFDJ_CN(H, N)                                                                       \
   hipLaunchKernelGGL((cn_update_kernel<STAGE, H, N>), g, b, 0, stream, w, jA, jB, out, kx, nx, \
-                     ny, hdt, re, alpha, cA, cB)
+                     ny, hdt, re, alpha, cA, cB, extra())
     if (half && stream_loads) CFDJ_CN(true, true);
     else if (half) CFDJ_CN(true, false);
     else if (stream_loads) CFDJ_CN(false, true);
@@ -767,10 +811,10 @@ struct cfdj_spec {
     if (half) {
       if (kind == CFDJ_SPEC_HYBRID)
         hipLaunchKernelGGL(full_to_half_kernel<true>, dim3(grid_for(nh())), dim3(256), 0, stream,
-                           full, dst, nx, ny);
+                           full, dst, nx, ny, 0);
       else
         hipLaunchKernelGGL(full_to_half_kernel<false>, dim3(grid_for(nh())), dim3(256), 0, stream,
-                           full, dst, nx, ny);
+                           full, dst, nx, ny, extra());
       CFDJ_HIP(hipGetLastError());
     } else if (kind == CFDJ_SPEC_HYBRID) {
       // hybrid.jl:103,115 sees w_f through real(ifft(.)) of w_f and w_f / k2 (k2 even), i.e.
@@ -786,7 +830,7 @@ struct cfdj_spec {
   void export_spectrum(const double2* src, double2* full) {
     if (half) {
       hipLaunchKernelGGL(half_to_full_kernel, dim3(grid_for(n())), dim3(256), 0, stream, src,
-                         full, nx, ny);
+                         full, nx, ny, extra());
       CFDJ_HIP(hipGetLastError());
     } else {
       CFDJ_HIP(hipMemcpyAsync(full, src, n() * sizeof(double2), hipMemcpyDeviceToDevice, stream));
@@ -875,15 +919,6 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     const char* re_ = std::getenv("CFDJ_SPEC_REAL");
     const bool want_real = !(re_ && re_[0] == '0');
     h->real_fields = h->hand_n && h->px == nx && want_real;
-    const char* he = std::getenv("CFDJ_SPEC_HALF");
-    h->half = want_hand && want_real && h->px == nx && half2d_supported(nx, ny) &&
-              !(he && he[0] == '0');
-    if (h->half) {
-      h->fz.init(nx, ny);
-      const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
-      h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,
-                           ny - nye / 2, h->stream_loads};
-    }
     h->real32 = kind == CFDJ_SPEC_PS32 && want_hand && want_real;
     const char* h32 = std::getenv("CFDJ_SPEC_PS32_HAND");
     h->hand32 = h->real32 && real2d3_supported(h->px) && nx % 16 == 0 &&
@@ -895,6 +930,19 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
       h->tw3_m3 = twiddle_table(h->px / 3);
       h->a3 = Real2d3Args{h->px, nx / 2, h->tw3_l3, h->tw3_l, h->tw3_n, h->tw3_m3,
                           h->stream_loads};
+      const double sc = (double)h->px * h->py, sd = (double)nx * ny;
+      h->s3 = Ps32HalfArgs{h->kx, sc / sd, sd / sc};
+    }
+    // half-spectrum state: the solvers whose product grid is the grid itself, and the 3/2 rule
+    // where its padded grid has the hand-written 3 * 2^k transforms
+    const char* he = std::getenv("CFDJ_SPEC_HALF");
+    h->half = want_hand && want_real && (h->px == nx || h->hand32) && half2d_supported(nx, ny) &&
+              !(he && he[0] == '0');
+    if (h->half) {
+      h->fz.init(nx, ny);
+      const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
+      h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,
+                           ny - nye / 2, h->stream_loads};
     }
     if (h->real_fields || h->half || h->real32) {
       h->R = dalloc<double>((size_t)nb * np);
@@ -944,6 +992,9 @@ int cfdj_spec_upload(cfdj_spec* h, const double* wn, long ldw) {
       CFDJ_HIP(hipMemcpy2DAsync(h->Rj, nx * sizeof(double), h->field, (nx + 1) * sizeof(double),
                                 nx * sizeof(double), ny, hipMemcpyDeviceToDevice, h->stream));
       launch_half_r2c2d(h->ha, h->Rj, h->X, h->wn, h->stream);
+      if (h->extra())
+        hipLaunchKernelGGL(ps32_fill_extra_kernel, dim3((nx / 2 + 256) / 256), dim3(256), 0,
+                           h->stream, h->wn, nx, ny);
     } else {
       hipLaunchKernelGGL(to_complex_kernel, dim3(grid_for(h->n())), dim3(256), 0, h->stream,
                          h->field, (long)(nx + 1), h->wn, nx, ny);
@@ -974,7 +1025,15 @@ int cfdj_spec_download(cfdj_spec* h, double* ut, long ldu) {
     const int nx = h->nx, ny = h->ny;
     const unsigned gf = grid_for((size_t)(nx + 1) * (ny + 1));
     if (h->half) {
-      launch_half_c2r2d(h->ha, kHalfPlain, h->wn, h->X, h->R, h->stream);
+      const double2* src = h->wn;
+      if (h->extra()) {  // j2 is scratch between steps
+        CFDJ_HIP(hipMemcpyAsync(h->j2, h->wn, (h->nh() + h->extra()) * sizeof(double2),
+                                hipMemcpyDeviceToDevice, h->stream));
+        hipLaunchKernelGGL(ps32_project_row_kernel, dim3((nx / 2 + 256) / 256), dim3(256), 0,
+                           h->stream, h->j2, nx, ny);
+        src = h->j2;
+      }
+      launch_half_c2r2d(h->ha, kHalfPlain, src, h->X, h->R, h->stream);
       hipLaunchKernelGGL(to_field_real_kernel, dim3(gf), dim3(256), 0, h->stream, h->R,
                          h->field, (long)(nx + 1), nx, ny, 1.0 / ((double)nx * ny));
     } else {
