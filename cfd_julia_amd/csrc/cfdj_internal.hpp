@@ -331,9 +331,17 @@ struct Ps32HalfArgs {
   double scale_in;    // (nxe nye) / (nx ny)
   double scale_out;   // (nx ny) / (nxe nye)
 };
-// r[b] = real(ifft2(padded derivative spectrum b of hs)), b < 4; x: 4 x (mmax + 1) x n scratch.
+// x[b] = the padded derivative spectrum b of hs, b < 4, transformed along y (4 x (mmax + 1) x n);
+// r[b] = real(ifft2(.)) of the first `nrow` of them (the inverse row pass).
 void launch_ps32_c2r2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double2* hs, double2* x,
-                        double* r, hipStream_t st);
+                        double* r, int nrow, hipStream_t st);
+// hs = unpadded fft2((r[0] r[1] - r[2] real(ifft_x(x4))) inv_np^2): the fourth field's inverse row
+// pass, the product (pseudospectral_32_rule.jl:156-169) and its forward transform, the rows in
+// one kernel.  x4: that field's (mmax + 1) x n array from launch_ps32_c2r2d3; r: three n x n
+// real arrays; xj: (mmax + 1) x n scratch.
+void launch_ps32_product_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double2* x4,
+                                const double* r, double2* xj, double2* hs, double inv_np,
+                                hipStream_t st);
 // hs = unpadded fft2(r) (columns 0..N/2); x: (mmax + 1) x n scratch.
 void launch_ps32_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double* r, double2* x,
                         double2* hs, hipStream_t st);

@@ -276,8 +276,8 @@ __global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_ps32_out
 // Pair i of a thread in a row workgroup of XR teams: row qq, columns m and L - m; 16
 // consecutive lanes take 16 consecutive m of one row (whole XR * 16-B column segments).
 template <int L3, int XR>
-__device__ __forceinline__ void pair3(int i, int& qq, int& m) {
-  const int e = threadIdx.x + i * (XR * Cfg3<L3>::TT);
+__device__ __forceinline__ void pair3(int tx, int i, int& qq, int& m) {
+  const int e = tx + i * (XR * Cfg3<L3>::TT);
   qq = (e >> 4) % XR;
   m = ((e >> 4) / XR) * 16 + (e & 15);
 }
@@ -292,18 +292,19 @@ __device__ __forceinline__ void pair3(int i, int& qq, int& m) {
 #else
 #define CFDJ_ROWS3_INV_ATTR
 #endif
-template <int L3, int XR, bool NTS>
-__global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_inv_kernel(
-    const double2* __restrict__ H, double* __restrict__ f, int M, int mmax,
-    const double2* __restrict__ tw3, const double2* __restrict__ twL,
-    const double2* __restrict__ twN) {
+
+// The rows y0 .. y0 + XR - 1 of the half spectrum H (M rows, columns 0..mmax) -> the thread's
+// 16 complex outputs o[j] = (f[2p], f[2p + 1]), p = tid + T3 j + q L3, of row y0 + team.
+template <int L3, int XR>
+__device__ __forceinline__ void c2r_rows3(const double2* __restrict__ H, int M, int mmax, int y0,
+                                          double* lds, int tx, const double2* __restrict__ tw3,
+                                          const double2* __restrict__ twL,
+                                          const double2* __restrict__ twN, double2 (&o)[16]) {
   using C = Cfg3<L3>;
   constexpr int L = C::L, THREADS = XR * C::TT, PAIRS = (L / 2) * XR / THREADS;
   static_assert(PAIRS * THREADS == (L / 2) * XR, "pair mapping");
-  __shared__ double lds[XR * C::PADL];
-  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  const int team = tx / C::TT, t = tx % C::TT, q = t / C::T3, tid = t % C::T3;
   double* buf = lds + team * C::PADL;
-  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
   const double2* base = H + __builtin_amdgcn_readfirstlane(y0);
   // c2r pre-processing of the pairs (m, L - m): Z[m] = (X[m] + conj X[L-m]) + i W_N^-m (X[m] -
   // conj X[L-m]); slot 0 = X[0] (the Nyquist mode of this grid is zero), Z[L/2] = 2 conj X[L/2]
@@ -313,7 +314,7 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
 #pragma unroll
   for (int i = 0; i < PAIRS; ++i) {
     int qq, m;
-    pair3<L3, XR>(i, qq, m);
+    pair3<L3, XR>(tx, i, qq, m);
     const bool z0 = i == 0 && m == 0;
     const int mq = z0 ? L / 2 : L - m;
     double2 Xm = make_double2(0.0, 0.0), Xq = Xm;
@@ -339,7 +340,7 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
       int qq, m;
-      pair3<L3, XR>(i, qq, m);
+      pair3<L3, XR>(tx, i, qq, m);
       double* bq = lds + qq * C::PADL;
       bq[padx(m)] = c ? o1[i].y : o1[i].x;
       bq[padx(i == 0 && m == 0 ? L / 2 : L - m)] = c ? o2[i].y : o2[i].x;
@@ -353,30 +354,39 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
     }
   }
   sub_fft<L3, 1>(buf, v, q, tid, tw3);
-  double2 o[16];
   combine3<L3, 1>(buf, v, q, tid, twL, o);
+}
+
+template <int L3, int XR, bool NTS>
+__global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_inv_kernel(
+    const double2* __restrict__ H, double* __restrict__ f, int M, int mmax,
+    const double2* __restrict__ tw3, const double2* __restrict__ twL,
+    const double2* __restrict__ twN) {
+  using C = Cfg3<L3>;
+  constexpr int L = C::L;
+  __shared__ double lds[XR * C::PADL];
+  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  double2 o[16];
+  c2r_rows3<L3, XR>(H, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN, o);
   double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + team) * (2 * L));
 #pragma unroll
   for (int j = 0; j < 16; ++j) store_stream<NTS>(z + tid + C::T3 * j + q * L3, o[j]);
 }
 
 // ---- rows, real -> half spectrum (r2c): XR rows per workgroup ------------------------------
-template <int L3, int XR, bool NT>
-__global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_fwd_kernel(
-    const double* __restrict__ f, double2* __restrict__ H, int M, int mmax,
-    const double2* __restrict__ tw3, const double2* __restrict__ twL,
-    const double2* __restrict__ twN) {
+// The thread's decimated inputs v[r] = (f[2p], f[2p + 1]), p = 3 (tid + T3 r) + q, of row
+// y0 + team -> the columns 0..mmax of rows y0 .. y0 + XR - 1 of the half spectrum H.
+template <int L3, int XR>
+__device__ __forceinline__ void r2c_rows3(double2 (&v)[16], double2* __restrict__ H, int M,
+                                          int mmax, int y0, double* lds, int tx,
+                                          const double2* __restrict__ tw3,
+                                          const double2* __restrict__ twL,
+                                          const double2* __restrict__ twN) {
   using C = Cfg3<L3>;
   constexpr int L = C::L, THREADS = XR * C::TT, PAIRS = (L / 2) * XR / THREADS;
-  __shared__ double lds[XR * C::PADL];
-  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  const int team = tx / C::TT, t = tx % C::TT, q = t / C::T3, tid = t % C::T3;
   double* buf = lds + team * C::PADL;
-  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
-  const double2* z = reinterpret_cast<const double2*>(f) + (size_t)(y0 + team) * L;
-  double2 v[16];
-  // the three sub-teams' loads interleave element by element: together whole lines
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = load_stream<NT>(z + 3 * (tid + C::T3 * r) + q);
   sub_fft<L3, -1>(buf, v, q, tid, tw3);
   double2 o[16];
   combine3<L3, -1>(buf, v, q, tid, twL, o);
@@ -392,7 +402,7 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
       int qq, m;
-      pair3<L3, XR>(i, qq, m);
+      pair3<L3, XR>(tx, i, qq, m);
       const double* bq = lds + qq * C::PADL;
       const double a = bq[padx(m)], b = bq[padx(i == 0 && m == 0 ? L / 2 : L - m)];
       if (c) {
@@ -410,7 +420,7 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
 #pragma unroll
   for (int i = 0; i < PAIRS; ++i) {
     int qq, m;
-    pair3<L3, XR>(i, qq, m);
+    pair3<L3, XR>(tx, i, qq, m);
     const bool z0 = i == 0 && m == 0;
     const int mp = z0 ? L / 2 : L - m;
     const double2 Zc = cconj(Zp[i]);
@@ -427,6 +437,97 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
     }
     if (m <= mmax) hb[(size_t)m * M + qq] = o1;
     if (mp <= mmax) hb[(size_t)mp * M + qq] = o2;
+  }
+}
+
+template <int L3, int XR, bool NT>
+__global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_fwd_kernel(
+    const double* __restrict__ f, double2* __restrict__ H, int M, int mmax,
+    const double2* __restrict__ tw3, const double2* __restrict__ twL,
+    const double2* __restrict__ twN) {
+  using C = Cfg3<L3>;
+  constexpr int L = C::L;
+  __shared__ double lds[XR * C::PADL];
+  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  const double2* z = reinterpret_cast<const double2*>(f) + (size_t)(y0 + team) * L;
+  double2 v[16];
+  // the three sub-teams' loads interleave element by element: together whole lines
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] = load_stream<NT>(z + 3 * (tid + C::T3 * r) + q);
+  r2c_rows3<L3, XR>(v, H, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN);
+}
+
+// ---- rows of the 3/2-rule solver's product (pseudospectral_32_rule.jl:156-169) ---------------
+// The fourth field's inverse row pass, the product j1 j2 - j3 j4 with the three fields already
+// in physical space (R: three arrays of n x n reals) and the product's forward row pass in one
+// kernel: a row of the fourth field and of the product never leaves the workgroup.  Each
+// factor is scaled by inv_np = 1 / (nxe nye) first, as the reference's ifft does.
+#ifndef CFDJ_ROWS3_JAC_WAVES
+#define CFDJ_ROWS3_JAC_WAVES 3
+#endif
+template <int L3, int XR, bool NT>
+__global__ __launch_bounds__((XR * Cfg3<L3>::TT))
+    __attribute__((amdgpu_waves_per_eu(CFDJ_ROWS3_JAC_WAVES, CFDJ_ROWS3_JAC_WAVES))) void rows3_jac_kernel(
+        const double2* __restrict__ H4, const double* __restrict__ R, double2* __restrict__ Hout,
+        int M, int mmax, double inv_np, const double2* __restrict__ tw3,
+        const double2* __restrict__ twL, const double2* __restrict__ twN) {
+  using C = Cfg3<L3>;
+  constexpr int L = C::L;
+  __shared__ double lds[XR * C::PADL];
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  double2 o[16];
+  c2r_rows3<L3, XR>(H4, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN, o);
+  // Each phase below works from its own opaque copy of the thread index, so that what depends
+  // only on it (pair offsets, buffer addresses, twiddles) is formed again where it is used
+  // instead of staying in registers from the inverse transform to the forward one; and the
+  // product's loads stay behind the inverse transform.
+  __builtin_amdgcn_sched_barrier(0);
+  int tx = threadIdx.x;
+  asm volatile("" : "+v"(tx));
+  {
+    const int team = tx / C::TT, t = tx % C::TT, q = t / C::T3, tid = t % C::T3;
+    const size_t full = (size_t)M * M;
+    const double2* r1 = reinterpret_cast<const double2*>(R) + (size_t)(y0 + team) * L + tid + q * L3;
+    const double2* r2 = r1 + full / 2;
+    const double2* r3 = r2 + full / 2;
+#pragma unroll
+    for (int j0 = 0; j0 < 16; j0 += 4) {
+      double2 a[4], b[4], c[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a[u] = load_stream<NT>(r1 + C::T3 * (j0 + u));
+        b[u] = load_stream<NT>(r2 + C::T3 * (j0 + u));
+        c[u] = load_stream<NT>(r3 + C::T3 * (j0 + u));
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        double2& d = o[j0 + u];
+        d.x = (a[u].x * inv_np) * (b[u].x * inv_np) - (c[u].x * inv_np) * (d.x * inv_np);
+        d.y = (a[u].y * inv_np) * (b[u].y * inv_np) - (c[u].y * inv_np) * (d.y * inv_np);
+      }
+    }
+    // the product row, natural order -> the forward sub-transforms' decimated inputs
+    double* buf = lds + team * C::PADL;
+    double2 v[16];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < 16; ++j) buf[padx(tid + C::T3 * j + q * L3)] = c ? o[j].y : o[j].x;
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const double a = buf[padx(3 * (tid + C::T3 * r) + q)];
+        if (c) v[r].y = a;
+        else v[r].x = a;
+      }
+    }
+    __syncthreads();  // the buffer's readers, before the sub-transforms' exchanges write it
+    __builtin_amdgcn_sched_barrier(0);
+    int tx2 = tx;
+    asm volatile("" : "+v"(tx2));
+    r2c_rows3<L3, XR>(v, Hout, M, mmax, y0, lds, tx2, tw3, twL, twN);
   }
 }
 
@@ -464,6 +565,22 @@ void launch_rows3(bool fwd, const Real2d3Args& a, const double* fin, double* fou
   }
 }
 
+#ifndef CFDJ_ROWS3_JAC_XR
+#define CFDJ_ROWS3_JAC_XR 4
+#endif
+template <int L3>
+void launch_rows3_jac(const Real2d3Args& a, const double2* x4, const double* r, double2* xj,
+                      double inv_np, hipStream_t st) {
+  constexpr int XJ = CFDJ_ROWS3_JAC_XR * Cfg3<L3>::TT <= 1024 ? CFDJ_ROWS3_JAC_XR : CFDJ_ROWS3_XR;
+  const dim3 grid(a.n / XJ), block(XJ * Cfg3<L3>::TT);
+  if (a.stream)
+    hipLaunchKernelGGL((rows3_jac_kernel<L3, XJ, true>), grid, block, 0, st, x4, r, xj, a.n, a.mmax,
+                       inv_np, a.tw3L, a.twL, a.twN);
+  else
+    hipLaunchKernelGGL((rows3_jac_kernel<L3, XJ, false>), grid, block, 0, st, x4, r, xj, a.n,
+                       a.mmax, inv_np, a.tw3L, a.twL, a.twN);
+}
+
 template <int M3>
 void launch_cols3(bool fwd, const Real2d3Args& a, double2* x, int batch, hipStream_t st) {
   const int ncols = a.mmax + 1;
@@ -486,7 +603,7 @@ void launch_cols3_ps32(bool fwd, const Real2d3Args& a, const Ps32HalfArgs& s, co
 
 void check3(const Real2d3Args& a) {
   if (!real2d3_supported(a.n) || a.mmax < 0 || a.mmax >= a.n / 2 || a.n % CFDJ_ROWS3_XR != 0 ||
-      a.n % CFDJ_ROWS3_FWD_XR != 0)
+      a.n % CFDJ_ROWS3_FWD_XR != 0 || a.n % CFDJ_ROWS3_JAC_XR != 0)
     throw Error{CFDJ_ERR_ARG, "3 * 2^k transform: unsupported size"};
 }
 
@@ -539,8 +656,9 @@ static void check_ps32(const Real2d3Args& a) {
 }
 
 void launch_ps32_c2r2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double2* hs, double2* x,
-                        double* r, hipStream_t st) {
+                        double* r, int nrow, hipStream_t st) {
   check_ps32(a);
+  if (nrow < 0 || nrow > 4) throw Error{CFDJ_ERR_ARG, "3/2-rule transform: bad array count"};
   const size_t half = (size_t)(a.mmax + 1) * a.n, full = (size_t)a.n * a.n;
   switch (a.n) {
     case 1536: launch_cols3_ps32<512>(false, a, s, hs, x, st); break;
@@ -548,7 +666,7 @@ void launch_ps32_c2r2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const doubl
     default: launch_cols3_ps32<2048>(false, a, s, hs, x, st); break;
   }
   CFDJ_HIP(hipGetLastError());
-  for (int b = 0; b < 4; ++b) {
+  for (int b = 0; b < nrow; ++b) {
     switch (a.n) {
       case 1536: launch_rows3<256>(false, a, nullptr, r + b * full, x + b * half, st); break;
       case 3072: launch_rows3<512>(false, a, nullptr, r + b * full, x + b * half, st); break;
@@ -573,6 +691,27 @@ void launch_ps32_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const doubl
     default:
       launch_rows3<1024>(true, a, r, nullptr, x, st);
       launch_cols3_ps32<2048>(true, a, s, x, hs, st);
+      break;
+  }
+  CFDJ_HIP(hipGetLastError());
+}
+
+void launch_ps32_product_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double2* x4,
+                                const double* r, double2* xj, double2* hs, double inv_np,
+                                hipStream_t st) {
+  check_ps32(a);
+  switch (a.n) {
+    case 1536:
+      launch_rows3_jac<256>(a, x4, r, xj, inv_np, st);
+      launch_cols3_ps32<512>(true, a, s, xj, hs, st);
+      break;
+    case 3072:
+      launch_rows3_jac<512>(a, x4, r, xj, inv_np, st);
+      launch_cols3_ps32<1024>(true, a, s, xj, hs, st);
+      break;
+    default:
+      launch_rows3_jac<1024>(a, x4, r, xj, inv_np, st);
+      launch_cols3_ps32<2048>(true, a, s, xj, hs, st);
       break;
   }
   CFDJ_HIP(hipGetLastError());

@@ -649,6 +649,7 @@ struct cfdj_spec {
   // 3 * 2^k transforms on the columns 0..nx/2 of that half spectrum (fft2d_r2c3.hip;
   // CFDJ_SPEC_PS32_HAND=0 keeps the library)
   bool hand32 = false;
+  bool fuse32 = true;  // CFDJ_SPEC_PS32_FUSE=0: the product as a kernel of its own
   Real2d3Args a3{};
   Ps32HalfArgs s3{};
   double2 *tw3_l3 = nullptr, *tw3_l = nullptr, *tw3_n = nullptr, *tw3_m3 = nullptr;
@@ -697,8 +698,15 @@ struct cfdj_spec {
                            1.0 / (4.0 * dx * dy), 1.0 / 3.0);
       } else if (kind == CFDJ_SPEC_PS32) {
         // padding, derivative factors and unpadding inside the column passes of the padded grid
-        launch_ps32_c2r2d3(a3, s3, wf, X, R, stream);
-        product_real(gb, 1.0 / ((double)px * py));
+        const double inv_np = 1.0 / ((double)px * py);
+        if (fuse32) {  // the fourth field's rows, the product and its row transform in one kernel
+          launch_ps32_c2r2d3(a3, s3, wf, X, R, 3, stream);
+          launch_ps32_product_r2c2d3(a3, s3, X + 3 * (size_t)(nx / 2 + 1) * py, R, J, jf, inv_np,
+                                     stream);
+          return;
+        }
+        launch_ps32_c2r2d3(a3, s3, wf, X, R, 4, stream);
+        product_real(gb, inv_np);
         CFDJ_HIP(hipGetLastError());
         launch_ps32_r2c2d3(a3, s3, Rj, J, jf, stream);
         return;
@@ -932,6 +940,8 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
                           h->stream_loads};
       const double sc = (double)h->px * h->py, sd = (double)nx * ny;
       h->s3 = Ps32HalfArgs{h->kx, sc / sd, sd / sc};
+      const char* f32 = std::getenv("CFDJ_SPEC_PS32_FUSE");
+      h->fuse32 = !(f32 && f32[0] == '0');
     }
     // half-spectrum state: the solvers whose product grid is the grid itself, and the 3/2 rule
     // where its padded grid has the hand-written 3 * 2^k transforms
