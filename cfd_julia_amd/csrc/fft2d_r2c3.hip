@@ -70,19 +70,34 @@ __device__ __forceinline__ void sub_fft(double* team_buf, double2 (&v)[16], int 
   run_stages_half<L3, 1, DIR>(team_buf + q * Cfg3<L3>::PAD3, v, tid, tw3);
 }
 
-// The radix-3 step: the three sub-transforms' outputs F_r[k] (in v, r = q) -> out[j] =
-// X[p], p = k + q L3, k = tid + T3 j: a thread's outputs are contiguous in p across the
-// lanes of its sub-team.  The F_r go through the team buffer one component at a time (F_r[k]
-// at r L3 + k); X[p] = F_0 + c1 F_1 + c2 F_2 with c1 = W_L^p, c2 = W_L^2p (conjugated for the
-// inverse), accumulated per component.
+// The radix-3 step: the three sub-transforms' outputs F_r[k] (in v, r = q) -> the team's
+// L3 radix-3 butterflies X[k + s L3] = F_0[k] + w3^s W_L^k F_1[k] + w3^2s W_L^2k F_2[k], s < 3
+// (w3 = exp(-+2 pi i / 3); conjugated twiddles for the inverse).  Butterfly k belongs to the
+// team's thread tt = q T3 + tid = k mod TT: five butterflies per thread, k = tt + TT b, b < 5,
+// and a sixth (b = 5) in the first sub-team, q = 0 (L3 = 5 TT + T3).  out[3 b + s] =
+// X[tt + TT b + s L3]: consecutive lanes hold consecutive elements.  The F_r go through the
+// team buffer one component at a time (F_r[k] at r L3 + k).  W_L^k = W_L^tt times the
+// constant W_16^b (TT / L = 1/16): one table load per thread.
+// Offset of a thread's butterfly b from its butterfly 0.  Outside the first sub-team there is
+// no sixth: b = 5 maps to butterfly 0 again, so the register arrays are filled and used
+// without predication (a predicated element of a register array costs a select per element
+// and its registers twice); only stores of out[15..17] are guarded, by has3(b, q).
+template <int L3>
+__device__ __forceinline__ int boff3(int b, int q) {
+  return b < 5 ? Cfg3<L3>::TT * b : (q == 0 ? 5 * Cfg3<L3>::TT : 0);
+}
+__device__ __forceinline__ bool has3(int b, int q) { return b < 5 || q == 0; }
+
 template <int L3, int DIR>
 __device__ __forceinline__ void combine3(double* team_buf, const double2 (&v)[16], int q,
                                          int tid, const double2* __restrict__ twL,
-                                         double2 (&out)[16]) {
+                                         double2 (&out)[18]) {
   using C = Cfg3<L3>;
   using P = Plan<L3>;
+  static_assert(5 * C::TT + C::T3 == L3, "butterflies per thread");
   constexpr int SL = P::NSTAGES - 1;
   constexpr int RL = P::radix(SL);
+  const int tt = q * C::T3 + tid;
 #pragma unroll
   for (int c = 0; c < 2; ++c) {
     __syncthreads();  // the buffer's previous readers
@@ -92,26 +107,34 @@ __device__ __forceinline__ void combine3(double* team_buf, const double2 (&v)[16
       for (int r = 0; r < RL; ++r)
         team_buf[padx(q * L3 + out_pos<L3, SL>(tid, b, r))] = c ? v[b * RL + r].y : v[b * RL + r].x;
     __syncthreads();
-    // an opaque copy of the thread index per component: the twiddles are loaded again in the
-    // second pass instead of staying live (64 registers) across the exchange
-    int tk = tid;
-    asm volatile("" : "+v"(tk));
-    double2 cb = twL[tk + q * L3];  // W_L^p of the thread's first output
-    if (DIR > 0) cb.y = -cb.y;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int k = tk + C::T3 * j;
-      const double2 c1 = cmul(cb, make_double2(kC48[j], DIR < 0 ? -kS48[j] : kS48[j]));
-      const double2 c2 = cmul(c1, c1);
-      const double f0 = team_buf[padx(k)], f1 = team_buf[padx(L3 + k)],
-                   f2 = team_buf[padx(2 * L3 + k)];
-      if (c == 0) {
-        out[j] = make_double2(f0 + f1 * c1.x + f2 * c2.x, f1 * c1.y + f2 * c2.y);
-      } else {  // i f c = (-f c.y, f c.x)
-        out[j].x -= f1 * c1.y + f2 * c2.y;
-        out[j].y += f0 + f1 * c1.x + f2 * c2.x;
+    for (int b = 0; b < 6; ++b) {
+      const int k = tt + boff3<L3>(b, q);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        const double f = team_buf[padx(r * L3 + k)];
+        if (c) out[3 * b + r].y = f;
+        else out[3 * b + r].x = f;
       }
     }
+  }
+  double2 cb = twL[tt];  // W_L^tt
+  if (DIR > 0) cb.y = -cb.y;
+  constexpr double h3 = 0.8660254037844386;  // sqrt(3) / 2
+#pragma unroll
+  for (int b = 0; b < 6; ++b) {
+    // (b = 5 outside the first sub-team: butterfly 0 again with another twiddle -- unused)
+    const double2 w1 = cmul(cb, make_double2(kC16[b], DIR < 0 ? -kS16[b] : kS16[b]));
+    const double2 w2 = cmul(w1, w1);
+    const double2 f0 = out[3 * b], t1 = cmul(out[3 * b + 1], w1), t2 = cmul(out[3 * b + 2], w2);
+    const double2 sm = cadd(t1, t2), df = csub(t1, t2);
+    const double2 m = make_double2(f0.x - 0.5 * sm.x, f0.y - 0.5 * sm.y);
+    // -+ i (sqrt(3) / 2) (t1 - t2)
+    const double2 rot = DIR < 0 ? make_double2(h3 * df.y, -h3 * df.x)
+                                : make_double2(-h3 * df.y, h3 * df.x);
+    out[3 * b] = cadd(f0, sm);
+    out[3 * b + 1] = cadd(m, rot);
+    out[3 * b + 2] = csub(m, rot);
   }
 }
 
@@ -136,14 +159,17 @@ __global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_kernel(
   double2 v[16];
   // the three sub-teams' loads interleave element by element: together whole lines
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = col[3 * (tid + C::T3 * r) + q];
+  for (int r = 0; r < 16; ++r) v[r] = col[(unsigned)(3 * (tid + C::T3 * r) + q)];
   sub_fft<M3, DIR>(lds, v, q, tid, tw3);
-  double2 o[16];
+  double2 o[18];
   combine3<M3, DIR>(lds, v, q, tid, twM, o);
   // (the DC column of a real field's spectrum transforms to real values up to round-off; the
   // inverse row pass reads the real parts of column 0 only)
 #pragma unroll
-  for (int j = 0; j < 16; ++j) col[tid + C::T3 * j + q * M3] = o[j];
+  for (int b = 0; b < 6; ++b)
+    if (has3(b, q))
+#pragma unroll
+      for (int r = 0; r < 3; ++r) col[(unsigned)(t + C::TT * b + r * M3)] = o[3 * b + r];
 }
 
 // ---- columns of the 3/2-rule solver on the half spectrum of its unpadded grid ---------------
@@ -177,6 +203,9 @@ __device__ __forceinline__ void ps32_load_column(double2 (&v)[16], const double2
   constexpr int N = 2 * M3, H = M3;
   const bool fp = a0 < H;
   const double kxa = kx[a0], kxm = kx[(N - a0) & (N - 1)];
+  // the table's entries (Common.jl:190-199: kx[1] = eps, else h times the signed index) formed
+  // from kx[0] and kx[1] = h instead of two more loads per element
+  const double eps = kx[0], h = kx[1];
   const bool xder = arr == 0 || arr == 3, overk2 = arr == 0 || arr == 2;
 #pragma unroll
   for (int r = 0; r < 16; ++r) {
@@ -184,7 +213,8 @@ __device__ __forceinline__ void ps32_load_column(double2 (&v)[16], const double2
     const bool kept = p <= H || p >= 2 * H;
     const int j = p <= H ? p : p - H;  // (the middle third maps to a valid index, unused)
     const int jm = (N - j) & (N - 1);
-    const double kyj = kx[j], kym = kx[jm];
+    const double kyj = j == 0 ? eps : h * (double)(j < H ? j : j - N);
+    const double kym = jm == 0 ? eps : h * (double)(jm < H ? jm : jm - N);
     const double kap_p = fp && p != H ? (xder ? kxa : kyj) : 0.0;
     const double kap_m = p != 2 * H ? (xder ? kxm : kym) : 0.0;
     double2 u;  // kappa(a0, j) w_f(a0, j) - kappa(-a0, -j) conj(w_f(-a0, -j))
@@ -220,11 +250,14 @@ __global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_ps32_in_
   if (a0 == 0 || a0 == M3) ps32_load_column<M3, true>(v, col, ex, kx, a0, arr, q, tid, scale);
   else ps32_load_column<M3, false>(v, col, ex, kx, a0, arr, q, tid, scale);
   sub_fft<M3, 1>(lds, v, q, tid, tw3);
-  double2 o[16];
+  double2 o[18];
   combine3<M3, 1>(lds, v, q, tid, twM, o);
-  double2* out = x + ((size_t)arr * (M3 + 1) + a0) * C::L;
+  double2* out = x + ((size_t)arr * (M3 + 1) + a0) * C::L;  // (wave-uniform)
 #pragma unroll
-  for (int j = 0; j < 16; ++j) out[tid + C::T3 * j + q * M3] = o[j];
+  for (int b = 0; b < 6; ++b)
+    if (has3(b, q))
+#pragma unroll
+      for (int r = 0; r < 3; ++r) out[(unsigned)(t + C::TT * b + r * M3)] = o[3 * b + r];
 }
 
 // Forward column pass with the unpadding of pseudospectral_32_rule.jl:171-178 where the column
@@ -245,31 +278,34 @@ __global__ __launch_bounds__((Cfg3<M3>::TT)) CFDJ_COLS3_ATTR void cols3_ps32_out
   const int t = threadIdx.x, q = t / C::T3, tid = t % C::T3;
   double2 v[16];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = col[3 * (tid + C::T3 * r) + q];
+  for (int r = 0; r < 16; ++r) v[r] = col[(unsigned)(3 * (tid + C::T3 * r) + q)];
   sub_fft<M3, -1>(lds, v, q, tid, tw3);
-  double2 o[16];
+  double2 o[18];
   combine3<M3, -1>(lds, v, q, tid, twM, o);
   double2* out = hs + (size_t)a0 * N;
   double2* ex = hs + (size_t)(M3 + 1) * N;
+  // butterfly k = t + TT b holds the padded elements k (first third), k + M3 (middle third)
+  // and k + 2 M3 (last third)
   if (a0 != H) {
-    if (q != 1) {
-      double2* ob = out + tid + (q == 2 ? M3 : 0);
 #pragma unroll
-      for (int j = 0; j < 16; ++j) ob[C::T3 * j] = make_double2(o[j].x * scale, o[j].y * scale);
-    } else if (tid == 0) {
-      ex[a0] = make_double2(o[0].x * scale, -o[0].y * scale);
-    }
+    for (int b = 0; b < 6; ++b)
+      if (has3(b, q)) {
+        const int k = t + C::TT * b;
+        out[k] = make_double2(o[3 * b].x * scale, o[3 * b].y * scale);
+        out[k + M3] = make_double2(o[3 * b + 2].x * scale, o[3 * b + 2].y * scale);
+      }
+    if (t == 0) ex[a0] = make_double2(o[1].x * scale, -o[1].y * scale);  // element M3
   } else {
     // element p goes to j = -p of the first and the last third; the padding puts -b = N/2 in
     // the last third's twin only: element M3 -> j = N/2 (and ex[N/2], the same mode)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int p = tid + C::T3 * j + q * M3;
-      const double2 c = make_double2(o[j].x * scale, -o[j].y * scale);
-      if (q == 0) out[(N - p) & (N - 1)] = c;
-      else if (q == 2 && p != 2 * M3) out[C::L - p] = c;
-      else if (q == 1 && p == M3) out[H] = ex[H] = c;
-    }
+    for (int b = 0; b < 6; ++b)
+      if (has3(b, q)) {
+        const int k = t + C::TT * b;
+        out[(N - k) & (N - 1)] = make_double2(o[3 * b].x * scale, -o[3 * b].y * scale);
+        if (k != 0) out[M3 - k] = make_double2(o[3 * b + 2].x * scale, -o[3 * b + 2].y * scale);
+      }
+    if (t == 0) out[H] = ex[H] = make_double2(o[1].x * scale, -o[1].y * scale);
   }
 }
 
@@ -294,12 +330,13 @@ __device__ __forceinline__ void pair3(int tx, int i, int& qq, int& m) {
 #endif
 
 // The rows y0 .. y0 + XR - 1 of the half spectrum H (M rows, columns 0..mmax) -> the thread's
-// 16 complex outputs o[j] = (f[2p], f[2p + 1]), p = tid + T3 j + q L3, of row y0 + team.
+// complex outputs o[3 b + s] = (f[2p], f[2p + 1]), p = t + TT b + s L3 (t the thread's index in
+// its team; b < 5, and b = 5 where q = 0: combine3), of row y0 + team.
 template <int L3, int XR>
 __device__ __forceinline__ void c2r_rows3(const double2* __restrict__ H, int M, int mmax, int y0,
                                           double* lds, int tx, const double2* __restrict__ tw3,
                                           const double2* __restrict__ twL,
-                                          const double2* __restrict__ twN, double2 (&o)[16]) {
+                                          const double2* __restrict__ twN, double2 (&o)[18]) {
   using C = Cfg3<L3>;
   constexpr int L = C::L, THREADS = XR * C::TT, PAIRS = (L / 2) * XR / THREADS;
   static_assert(PAIRS * THREADS == (L / 2) * XR, "pair mapping");
@@ -318,8 +355,8 @@ __device__ __forceinline__ void c2r_rows3(const double2* __restrict__ H, int M, 
     const bool z0 = i == 0 && m == 0;
     const int mq = z0 ? L / 2 : L - m;
     double2 Xm = make_double2(0.0, 0.0), Xq = Xm;
-    if (m <= mmax) Xm = base[(size_t)m * M + qq];
-    if (mq <= mmax) Xq = base[(size_t)mq * M + qq];
+    if (m <= mmax) Xm = base[(unsigned)(m * M + qq)];
+    if (mq <= mmax) Xq = base[(unsigned)(mq * M + qq)];
     const double2 Xp = cconj(Xq);
     const double2 S = cadd(Xm, Xp);
     if (i == 0) wn0 = cconj(twN[m]);  // W_N^-m of pair 0; pair i: m + TT i
@@ -367,11 +404,16 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
   __shared__ double lds[XR * C::PADL];
   const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
   const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
-  double2 o[16];
+  double2 o[18];
   c2r_rows3<L3, XR>(H, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN, o);
-  double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + team) * (2 * L));
+  // (a wave-uniform base and 32-bit element offsets: one offset register per access)
+  double2* z = reinterpret_cast<double2*>(f) + (size_t)__builtin_amdgcn_readfirstlane(y0) * L;
 #pragma unroll
-  for (int j = 0; j < 16; ++j) store_stream<NTS>(z + tid + C::T3 * j + q * L3, o[j]);
+  for (int b = 0; b < 6; ++b)
+    if (has3(b, q))
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+        store_stream<NTS>(z + (unsigned)(team * L + t + C::TT * b + r * L3), o[3 * b + r]);
 }
 
 // ---- rows, real -> half spectrum (r2c): XR rows per workgroup ------------------------------
@@ -388,7 +430,7 @@ __device__ __forceinline__ void r2c_rows3(double2 (&v)[16], double2* __restrict_
   const int team = tx / C::TT, t = tx % C::TT, q = t / C::T3, tid = t % C::T3;
   double* buf = lds + team * C::PADL;
   sub_fft<L3, -1>(buf, v, q, tid, tw3);
-  double2 o[16];
+  double2 o[18];
   combine3<L3, -1>(buf, v, q, tid, twL, o);
   // natural order through the buffer, read back as the pairs (m, L - m) of the r2c
   // post-processing
@@ -397,7 +439,11 @@ __device__ __forceinline__ void r2c_rows3(double2 (&v)[16], double2* __restrict_
   for (int c = 0; c < 2; ++c) {
     __syncthreads();
 #pragma unroll
-    for (int j = 0; j < 16; ++j) buf[padx(tid + C::T3 * j + q * L3)] = c ? o[j].y : o[j].x;
+    for (int b = 0; b < 6; ++b)
+      if (has3(b, q))
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+          buf[padx(t + C::TT * b + r * L3)] = c ? o[3 * b + r].y : o[3 * b + r].x;
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < PAIRS; ++i) {
@@ -435,8 +481,8 @@ __device__ __forceinline__ void r2c_rows3(double2 (&v)[16], double2* __restrict_
       o1 = make_double2(Zm[i].x + Zm[i].y, 0.0);
       o2 = Zc;
     }
-    if (m <= mmax) hb[(size_t)m * M + qq] = o1;
-    if (mp <= mmax) hb[(size_t)mp * M + qq] = o2;
+    if (m <= mmax) hb[(unsigned)(m * M + qq)] = o1;
+    if (mp <= mmax) hb[(unsigned)(mp * M + qq)] = o2;
   }
 }
 
@@ -450,11 +496,13 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3
   __shared__ double lds[XR * C::PADL];
   const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
   const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
-  const double2* z = reinterpret_cast<const double2*>(f) + (size_t)(y0 + team) * L;
+  const double2* z =
+      reinterpret_cast<const double2*>(f) + (size_t)__builtin_amdgcn_readfirstlane(y0) * L;
   double2 v[16];
   // the three sub-teams' loads interleave element by element: together whole lines
 #pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] = load_stream<NT>(z + 3 * (tid + C::T3 * r) + q);
+  for (int r = 0; r < 16; ++r)
+    v[r] = load_stream<NT>(z + (unsigned)(team * L + 3 * (tid + C::T3 * r) + q));
   r2c_rows3<L3, XR>(v, H, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN);
 }
 
@@ -476,7 +524,7 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT))
   constexpr int L = C::L;
   __shared__ double lds[XR * C::PADL];
   const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
-  double2 o[16];
+  double2 o[18];
   c2r_rows3<L3, XR>(H4, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN, o);
   // Each phase below works from its own opaque copy of the thread index, so that what depends
   // only on it (pair offsets, buffer addresses, twiddles) is formed again where it is used
@@ -488,23 +536,28 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT))
   {
     const int team = tx / C::TT, t = tx % C::TT, q = t / C::T3, tid = t % C::T3;
     const size_t full = (size_t)M * M;
-    const double2* r1 = reinterpret_cast<const double2*>(R) + (size_t)(y0 + team) * L + tid + q * L3;
+    const double2* r1 =
+        reinterpret_cast<const double2*>(R) + (size_t)__builtin_amdgcn_readfirstlane(y0) * L;
     const double2* r2 = r1 + full / 2;
     const double2* r3 = r2 + full / 2;
 #pragma unroll
-    for (int j0 = 0; j0 < 16; j0 += 4) {
-      double2 a[4], b[4], c[4];
+    for (int b = 0; b < 6; ++b) {
+      const unsigned kb = team * L + t + boff3<L3>(b, q);
+      double2 f1[3], f2[3], f3[3];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a[u] = load_stream<NT>(r1 + C::T3 * (j0 + u));
-        b[u] = load_stream<NT>(r2 + C::T3 * (j0 + u));
-        c[u] = load_stream<NT>(r3 + C::T3 * (j0 + u));
+      for (int u = 0; u < 3; ++u) {
+        f1[u] = load_stream<NT>(r1 + (kb + u * L3));
+        f2[u] = load_stream<NT>(r2 + (kb + u * L3));
+        f3[u] = load_stream<NT>(r3 + (kb + u * L3));
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        double2& d = o[j0 + u];
-        d.x = (a[u].x * inv_np) * (b[u].x * inv_np) - (c[u].x * inv_np) * (d.x * inv_np);
-        d.y = (a[u].y * inv_np) * (b[u].y * inv_np) - (c[u].y * inv_np) * (d.y * inv_np);
+      for (int u = 0; u < 3; ++u) {
+        double2& d = o[3 * b + u];
+        d.x = (f1[u].x * inv_np) * (f2[u].x * inv_np) - (f3[u].x * inv_np) * (d.x * inv_np);
+        d.y = (f1[u].y * inv_np) * (f2[u].y * inv_np) - (f3[u].y * inv_np) * (d.y * inv_np);
+        // formed here: left to the compiler, the imaginary parts are computed where the exchange
+        // below first uses them, and their 3 x 18 factors stay in registers until then
+        asm volatile("" : "+v"(d.x), "+v"(d.y));
       }
     }
     // the product row, natural order -> the forward sub-transforms' decimated inputs
@@ -514,7 +567,11 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT))
     for (int c = 0; c < 2; ++c) {
       __syncthreads();
 #pragma unroll
-      for (int j = 0; j < 16; ++j) buf[padx(tid + C::T3 * j + q * L3)] = c ? o[j].y : o[j].x;
+      for (int b = 0; b < 6; ++b)
+        if (has3(b, q))
+#pragma unroll
+          for (int u = 0; u < 3; ++u)
+            buf[padx(t + C::TT * b + u * L3)] = c ? o[3 * b + u].y : o[3 * b + u].x;
       __syncthreads();
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
