@@ -137,12 +137,18 @@ struct Plan {
   static constexpr int T = L / NV;  // threads per transform
   static constexpr int radix(int s) { return s < NFULL ? NV : REM; }
   static constexpr int ns(int s) { return s == 0 ? 1 : ns(s - 1) * radix(s - 1); }
+#ifdef CFDJ_LDS_PAD32
+  static constexpr int PAD = L + L / 32;  // LDS elements per transform (1 pad per 32)
+#else
   static constexpr int PAD = L + L / 16;  // LDS elements per transform (1 pad per 16)
+#endif
   static constexpr int ROWSTRIDE = PAD;  // rows kernels: row stride (= 0 mod 64 banks)
 };
 
-#ifdef CFDJ_LDS_XOR
+#if defined(CFDJ_LDS_XOR)
 __device__ __forceinline__ int padx(int i) { return i ^ ((i >> 4) & 15); }
+#elif defined(CFDJ_LDS_PAD32)
+__device__ __forceinline__ int padx(int i) { return i + (i >> 5); }
 #else
 __device__ __forceinline__ int padx(int i) { return i + (i >> 4); }
 #endif

@@ -194,27 +194,100 @@ def test_gpu_spectral_hand_fft_matches_library(spec, monkeypatch, kind, n):
         assert np.abs(spc[name] - spc["rocfft"]).max() <= 1e-12 * sscale, name
 
 
-@pytest.mark.parametrize("kind", ["hybrid", "2/3"])
+@pytest.mark.parametrize("kind", KINDS)
 def test_gpu_spectral_half_spectrum_round_trip(spec, kind):
     """set_spectrum / spectrum through the half-spectrum state (n = 1024), Nyquist row and
     column included, bit for bit: the hybrid solver returns the Hermitian part (w_f(k) +
     conj(w_f(-k))) / 2 of what went in -- for the spectrum of a real field the spectrum itself,
     up to the last-bit asymmetries of the CPU FFT that produced it -- the 2/3 rule the kx
-    columns 0..n/2 as given and their conjugate mirror."""
+    columns 0..n/2 as given and their conjugate mirror.  The 3/2 rule's state also carries the
+    row ky index n/2 of the other half as given: its unpadding (pseudospectral_32_rule.jl:
+    171-178) fills that row with the padded grid's mode -n/2, which is not the conjugate of
+    the row's first half, so the test makes the two halves of that row differ."""
     n = 1024
     dx, dy, _, _ = vo.vm_grid(n, n)
     f = smooth_field(n, n, 5, n) + 0.01 * np.random.default_rng(7).standard_normal((n, n))
     wf = so.to_spectral(f)
+    if kind == "3/2":
+        rng = np.random.default_rng(11)
+        wf[n // 2 + 1:, n // 2] += rng.standard_normal(n // 2 - 1) + 1j * rng.standard_normal(n // 2 - 1)
     with spec.SpectralNS2D(n, n, dx, dy, 1000.0, kind) as h:
         h.set_spectrum(wf)
         back = h.spectrum()
     mirror = np.conj(wf[(-np.arange(n)) % n][:, (-np.arange(n)) % n])
     herm = 0.5 * (wf + mirror) if kind == "hybrid" else wf
-    assert np.abs(herm - wf).max() <= 1e-15 * np.abs(wf).max()
+    if kind != "3/2":
+        assert np.abs(herm - wf).max() <= 1e-15 * np.abs(wf).max()
     i = np.arange(n // 2 + 1)
     assert np.array_equal(back[i, :], herm[i, :])
     hm = np.conj(herm[(-np.arange(n)) % n][:, (-np.arange(n)) % n])
+    if kind == "3/2":
+        hm[n // 2 + 1:, n // 2] = wf[n // 2 + 1:, n // 2]
     assert np.array_equal(back[n // 2 + 1:, :], hm[n // 2 + 1:, :])
+
+
+def _noisy_start(n):
+    """The vortex pair plus white noise: content in every mode, the Nyquist row and column
+    included, which the 3/2 rule's padding treats unsymmetrically."""
+    dx, dy, x, y = vo.vm_grid(n, n)
+    return vo.vm_ic(n, n, x, y) + 0.05 * np.random.default_rng(3 * n).standard_normal((n, n))
+
+
+def test_gpu_spectral_32_rule_noisy_steps_vs_oracle_1024(spec):
+    """pseudospectral_32_rule.jl on the half-spectrum state (n = 1024: padded grid 1536 = 3 *
+    2^9) against the oracle over 3 steps from a field with content in every mode: the state's
+    Nyquist row stops being Hermitian after the first Jacobian (the unpadding takes the padded
+    grid's mode -n/2 for it), which the half spectrum carries as an extra row.  Fields to
+    1e-10, the full spectrum through the C interface to 1e-12 of its maximum."""
+    n, steps, dt = 1024, 3, 1e-3
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    w0 = _noisy_start(n)
+    k2 = so.wavespace(n, n, dx, dy)
+    wf = so.to_spectral(w0)
+    for _ in range(steps):
+        wf = so.step(wf, k2, dt, 1000.0, dx, dy, so.PS32)
+    ref = so.to_physical(wf)
+    with spec.SpectralNS2D(n, n, dx, dy, 1000.0, "3/2") as h:
+        h.upload_interior(w0)
+        h.step(dt, steps)
+        ut = h.download()
+        got = h.spectrum()
+    # the oracle's state is not Hermitian on the Nyquist row: the test would not see a
+    # symmetrised state otherwise
+    hy = n // 2
+    asym = np.abs(wf[hy + 1:, hy] - np.conj(wf[1:hy, hy][::-1])).max()
+    assert asym > 1e-6 * np.abs(wf[:, hy]).max()
+    assert np.abs(ut[:n, :n] - ref).max() < 1e-10
+    assert np.abs(got - wf).max() <= 1e-12 * np.abs(wf).max()
+
+
+@pytest.mark.parametrize("n", [1024, 4096])
+def test_gpu_spectral_32_rule_variants_agree(spec, monkeypatch, n):
+    """The 3/2 rule's paths on the hand-written 3 * 2^k transforms give the same fields and
+    spectra to FFT round-off (1e-12 of the maximum, 2 steps from the noisy start): the
+    half-spectrum state with the product fused into the row passes (default), the product as
+    a kernel of its own (CFDJ_SPEC_PS32_FUSE=0), and the full-spectrum state with separate
+    derivative / unpadding kernels (CFDJ_SPEC_HALF=0)."""
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    w0 = _noisy_start(n)
+    out, spc = {}, {}
+    envs = ("CFDJ_SPEC_PS32_FUSE", "CFDJ_SPEC_HALF")
+    for name, env in (("fused", {}), ("unfused", {"CFDJ_SPEC_PS32_FUSE": "0"}),
+                      ("full", {"CFDJ_SPEC_HALF": "0"})):
+        for k in envs:
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, "3/2") as h:
+            h.upload_interior(w0)
+            h.step(2.5e-4, 2)
+            out[name] = h.download()
+            spc[name] = h.spectrum()
+    scale, sscale = np.abs(out["full"]).max(), np.abs(spc["full"]).max()
+    for name in ("fused", "unfused"):
+        assert np.isfinite(out[name]).all()
+        assert np.abs(out[name] - out["full"]).max() <= 1e-12 * scale, name
+        assert np.abs(spc[name] - spc["full"]).max() <= 1e-12 * sscale, name
 
 
 @pytest.mark.parametrize("kind", KINDS)
