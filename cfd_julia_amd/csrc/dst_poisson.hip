@@ -389,19 +389,29 @@ __global__ __launch_bounds__(DstNpCfg<M2>::THREADS) void dst_rows_fwd_np_kernel(
 #ifndef CFDJ_DST_COLS_WAVES
 #define CFDJ_DST_COLS_WAVES 3
 #endif
+// Values per thread (16 or 8): a pass has only nx / 2 columns (four per CU at 2048^2), so its
+// time is the latency of one column's chain of loads, stages and exchanges times the rounds
+// of resident workgroups -- twice the threads per column shorten that chain.
+#ifndef CFDJ_DST_COLS_NV
+#define CFDJ_DST_COLS_NV 16
+#endif
+constexpr int kDstNV = CFDJ_DST_COLS_NV;
 // Wavefronts per SIMD the kernel is compiled for (the register cap): one per resident
 // 256-thread workgroup at M2 = 4096.
 template <int M2>
-constexpr int dst_cols_waves() { return M2 <= 4096 ? CFDJ_DST_COLS_WAVES : 2; }
+constexpr int dst_cols_waves() {
+  return kDstNV == 8 ? 4 : (M2 <= 4096 ? CFDJ_DST_COLS_WAVES : 2);
+}
 
 template <int M2>
-__global__ __launch_bounds__(Plan<M2>::T)
+__global__ __launch_bounds__((Plan<M2, kDstNV>::T))
     __attribute__((amdgpu_waves_per_eu(dst_cols_waves<M2>(), dst_cols_waves<M2>()))) void dst_cols_kernel(double2* __restrict__ T, int JT,
                                                              const double* __restrict__ tx,
                                                              const double* __restrict__ ty,
                                                              double scale,
                                                              const double2* __restrict__ tw_) {
-  using PL = Plan<M2>;
+  constexpr int NV = kDstNV;
+  using PL = Plan<M2, NV>;
   static_assert(PL::NSTAGES >= 2, "column length");
   constexpr int ny = M2 / 2;
   __shared__ double lds[PL::PAD];  // one component at a time (exchange_half): 3 per CU
@@ -410,13 +420,13 @@ __global__ __launch_bounds__(Plan<M2>::T)
   const int kap = xcd_remap(blockIdx.x, gridDim.x);
   double2* col = T + (size_t)kap * JT;  // row j in slot j - 1
 
-  double2 a[16];
+  double2 a[NV];
   constexpr int R0 = PL::radix(0);
 #pragma unroll
-  for (int b = 0; b < 16 / R0; ++b)
+  for (int b = 0; b < NV / R0; ++b)
 #pragma unroll
     for (int r = 0; r < R0; ++r) {
-      const int p = in_pos<M2, 0>(tid, b, r);
+      const int p = in_pos<M2, 0, NV>(tid, b, r);
       const bool zero = (p & (ny - 1)) == 0;
       const int j = p < ny ? p : M2 - p;
       const double2 c = col[zero ? 0 : j - 1];
@@ -426,11 +436,11 @@ __global__ __launch_bounds__(Plan<M2>::T)
   stage_regs<M2, 0, -1>(a, tid, tw);
   run_stages_half<M2, 1, -1>(lds, a, tid, tw);  // last stage stays in registers
 
-  double2 v[16];
+  double2 v[NV];
   fwd_to_inv<M2>(a, v);  // v[r] = Z[p], p = tid + T r
   const double txa = tx[2 * kap], txb = tx[2 * kap + 1];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
+  for (int r = 0; r < NV; ++r) {
     const int p = tid + PL::T * r;
     const bool zero = (p & (ny - 1)) == 0;
     const double t = ty[p];  // even in p about ny (the table holds the extension)
@@ -446,10 +456,10 @@ __global__ __launch_bounds__(Plan<M2>::T)
   constexpr int SL = PL::NSTAGES - 1;
   constexpr int RL = PL::radix(SL);
 #pragma unroll
-  for (int b = 0; b < 16 / RL; ++b)
+  for (int b = 0; b < NV / RL; ++b)
 #pragma unroll
     for (int r = 0; r < RL; ++r) {
-      const int p = out_pos<M2, SL>(tid, b, r);
+      const int p = out_pos<M2, SL, NV>(tid, b, r);
       if (p >= 1 && p < ny) col[p - 1] = make_double2(-v[b * RL + r].y, v[b * RL + r].x);
     }
 }
@@ -499,7 +509,7 @@ void launch_dst_rows(int pass, const DstPoissonArgs& a, hipStream_t st) {
 
 template <int M2>
 void launch_dst_cols(const DstPoissonArgs& a, hipStream_t st) {
-  hipLaunchKernelGGL((dst_cols_kernel<M2>), dim3(a.nx / 2), dim3(Plan<M2>::T), 0, st, a.T, a.JT,
+  hipLaunchKernelGGL((dst_cols_kernel<M2>), dim3(a.nx / 2), dim3(Plan<M2, kDstNV>::T), 0, st, a.T, a.JT,
                      a.tx, a.ty, a.scale, a.twY);
 }
 
