@@ -232,6 +232,11 @@ bool fused_poisson_supported(int nx, int ny, int rows);
 bool fused_rows_take_col0(int nx, int rows);
 bool fused_rows_supported(int nx, int rows);  // the row passes alone (y-slab Schur path)
 void launch_fused_poisson_pass(int pass, const FusedPoissonArgs& a, hipStream_t st);
+// The 2/3-rule solver's product rows in one kernel (poisson_fft.hip, rows_jac_np_kernel):
+// inverse row pass of the scratch spectrum a.H (columns 0..a.mmax), product with the three
+// real fields at a.f, forward row pass into the scratch spectrum a.C; rows of up to 4096 reals.
+bool rows_jac_supported(int nx, int rows);
+void launch_rows_jac(const FusedPoissonArgs& a, double inv_np, hipStream_t st);
 
 // DST-I Poisson solve of the cavity on its own interior (dst_poisson.hip): pass 0 = x-DST of
 // the rows of w (sign folded in) -> T, pass 1 = y-DST, iden multiply, y-DST on T in place,
@@ -300,6 +305,13 @@ void launch_half_r2c2d(const HalfSpecArgs& a, const double* r, double2* scratch,
 // scratch.  hs is left intact.
 void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, double2* x, double* r,
                        hipStream_t st);
+// hs_out = fft2 (half) of the 2/3 rule's product r[0] r[1] - r[2] r[3], r[b] = real(ifft2(
+// factor_b(hs))) / n^2 as launch_half_c2r2d(kHalfPs23) forms them: the fourth field's rows, the
+// product and its row transform in one kernel (r: three n x n arrays are written).  Grids of
+// up to 4096^2 (half_ps23_jacobian_supported).
+bool half_ps23_jacobian_supported(int n);
+void launch_half_ps23_jacobian(const HalfSpecArgs& a, const double2* hs, double2* x, double* r,
+                               double2* hs_out, hipStream_t st);
 
 // 2-D transforms of REAL n-by-n fields with n = 3 * 2^k (1536, 3072, 6144: the 3/2 rule's
 // product grids) on the columns m = 0..mmax of the half spectrum (fft2d_r2c3.hip): element

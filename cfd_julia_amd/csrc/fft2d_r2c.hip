@@ -298,4 +298,28 @@ void launch_half_c2r2d(const HalfSpecArgs& a, int mode, const double2* hs, doubl
   }
 }
 
+bool half_ps23_jacobian_supported(int n) {
+  return half2d_supported(n, n) && band_limited(n) && rows_jac_supported(n, n);
+}
+
+void launch_half_ps23_jacobian(const HalfSpecArgs& a, const double2* hs, double2* x, double* r,
+                               double2* hs_out, hipStream_t st) {
+  check(a);
+  if (!half_ps23_jacobian_supported(a.n))
+    throw Error{CFDJ_ERR_ARG, "half-spectrum 2/3-rule product: unsupported size"};
+  const size_t half = (size_t)(a.n / 2) * a.n, full = (size_t)a.n * a.n;
+  half_cols(kHalfPs23, a, hs, x, 0, 4, st);
+  for (int b = 0; b < 3; ++b) {
+    FusedPoissonArgs p = row_args(a, nullptr, r + b * full, x + b * half);
+    p.mmax = a.tx0;
+    launch_fused_poisson_pass(2, p, st);
+  }
+  // the product's scratch spectrum goes where the first field's was (consumed above)
+  FusedPoissonArgs p = row_args(a, r, nullptr, x + 3 * half);
+  p.C = x;
+  p.mmax = a.tx0;
+  launch_rows_jac(p, 1.0 / ((double)a.n * a.n), st);
+  half_cols(0, a, x, hs_out, 0, 1, st);
+}
+
 }  // namespace cfdj

@@ -750,6 +750,166 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
   }
 }
 
+// The 2/3-rule solver's product rows (pseudospectral_23_rule.jl:134-140): the inverse row pass
+// of the fourth derivative field (band-limited half spectrum H4, column-major), the product
+// j1 j2 - j3 j4 with the three fields already in physical space (R: three arrays of M rows of
+// 2L reals), and the product's forward row pass (-> Hout, column-major packed half spectrum)
+// in one kernel: the fourth field and the product never reach HBM.  The inverse transform's
+// last stage leaves a thread the elements the forward transform's stage 0 reads (fwd_to_inv),
+// so the product is formed in registers with no exchange between the transforms.  Each factor
+// is scaled by inv_np = 1 / (nx ny) first, as the reference's ifft does.
+template <int L, int XR, bool NT>
+__global__ __launch_bounds__(XR* Plan<L>::T) void rows_jac_np_kernel(
+    const double2* __restrict__ H4, const double* __restrict__ R, double2* __restrict__ Hout,
+    int M, const double2* __restrict__ twL_, const double2* __restrict__ twN_, int mmax,
+    double inv_np) {
+  using P = Plan<L>;
+  constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
+  constexpr int SL = P::NSTAGES - 1;
+  constexpr int RL = P::radix(SL);
+  __shared__ double lds[XR * P::PAD];
+  const TwGlobal<L> twL{twL_};
+  const TwGlobal<2 * L> twN{twN_};
+  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  double2 v[16];
+  {  // ---- c2r of rows y0 .. y0 + XR - 1 of H4 (rows_inv_np_kernel's steps)
+    const int tx = threadIdx.x;
+    const int q = tx / P::T, tid = tx % P::T;
+    double* buf = lds + q * P::PAD;
+    const double2* base = H4 + __builtin_amdgcn_readfirstlane(y0);
+    double2 o1[PAIRS], o2[PAIRS];
+    auto pair = [tx](int i, int& qq, int& m) {
+      const int e = tx + i * THREADS;
+      qq = (e >> 4) % XR;
+      m = ((e >> 4) / XR) * 16 + (e & 15);
+    };
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      int qq, m;
+      pair(i, qq, m);
+      const bool z0 = i == 0 && m == 0;
+      const int mq = z0 ? L / 2 : L - m;
+      double2 Xm = make_double2(0.0, 0.0), Xq = Xm;
+      if (m <= mmax) Xm = base[(unsigned)(m * M + qq)];
+      if (mq <= mmax) Xq = base[(unsigned)(mq * M + qq)];
+      const double2 Xp = cconj(Xq);
+      const double2 S = cadd(Xm, Xp);
+      const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
+      o1[i] = make_double2(S.x - D.y, S.y + D.x);
+      o2[i] = make_double2(S.x + D.y, D.x - S.y);
+      if (z0) {  // slot 0 = (X[0], X[L]), both real; Z[L/2] = 2 conj(X[L/2])
+        o1[i] = make_double2(Xm.x + Xm.y, Xm.x - Xm.y);
+        o2[i] = make_double2(2.0 * Xq.x, -2.0 * Xq.y);
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      if (c) __syncthreads();
+#pragma unroll
+      for (int i = 0; i < PAIRS; ++i) {
+        int qq, m;
+        pair(i, qq, m);
+        double* bq = lds + qq * P::PAD;
+        bq[padx(m)] = c ? o1[i].y : o1[i].x;
+        bq[padx(i == 0 && m == 0 ? L / 2 : L - m)] = c ? o2[i].y : o2[i].x;
+      }
+      __syncthreads();
+      if (c) lds_read_half<L, 0, 1>(buf, v, tid);
+      else lds_read_half<L, 0, 0>(buf, v, tid);
+    }
+    stage_regs<L, 0, 1>(v, tid, twL);
+    run_stages_half<L, 1, 1>(buf, v, tid, twL);
+  }
+  // Each phase works from its own opaque copy of the thread index: what depends only on it
+  // (pair offsets, buffer addresses, twiddles) is formed again where it is used instead of
+  // staying in registers from one transform to the other; the product's loads stay behind
+  // the inverse transform.
+  __builtin_amdgcn_sched_barrier(0);
+  int tx = threadIdx.x;
+  asm volatile("" : "+v"(tx));
+  {  // ---- product: v = (f1 inv)(f2 inv) - (f3 inv)(v inv) at the thread's elements
+    const int q = tx / P::T, tid = tx % P::T;
+    const size_t full = (size_t)M * L;  // complex elements per real array
+    const double2* r1 = reinterpret_cast<const double2*>(R) +
+                        (size_t)__builtin_amdgcn_readfirstlane(y0) * L;
+    const double2* r2 = r1 + full;
+    const double2* r3 = r2 + full;
+#pragma unroll
+    for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+      for (int r = 0; r < RL; ++r) {
+        const unsigned off = (unsigned)(q * L + out_pos<L, SL>(tid, b, r));
+        const double2 f1 = load_stream<NT>(r1 + off), f2 = load_stream<NT>(r2 + off);
+        const double2 f3 = load_stream<NT>(r3 + off);
+        double2& d = v[b * RL + r];
+        d.x = (f1.x * inv_np) * (f2.x * inv_np) - (f3.x * inv_np) * (d.x * inv_np);
+        d.y = (f1.y * inv_np) * (f2.y * inv_np) - (f3.y * inv_np) * (d.y * inv_np);
+        // formed here, not where the next exchange first uses them (their factors would
+        // stay in registers until then)
+        asm volatile("" : "+v"(d.x), "+v"(d.y));
+      }
+  }
+  __builtin_amdgcn_sched_barrier(0);
+  int tx2 = tx;
+  asm volatile("" : "+v"(tx2));
+  {  // ---- r2c of the product rows (rows_fwd_np_kernel's steps)
+    const int q = tx2 / P::T, tid = tx2 % P::T;
+    double* buf = lds + q * P::PAD;
+    double2 a[16];
+    fwd_to_inv<L>(v, a);  // a[r] = element tid + T r
+    stage_regs<L, 0, -1>(a, tid, twL);
+    run_stages_half<L, 1, -1>(buf, a, tid, twL);
+    auto pair = [tx2](int i, int& qq, int& m) {
+      const int e = tx2 + i * THREADS;
+      qq = (e >> 4) % XR;
+      m = ((e >> 4) / XR) * 16 + (e & 15);
+    };
+    double2 Zm[PAIRS], Zp[PAIRS];
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      __syncthreads();
+      if (c) lds_write_half<L, SL, 1>(buf, a, tid);
+      else lds_write_half<L, SL, 0>(buf, a, tid);
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < PAIRS; ++i) {
+        int qq, m;
+        pair(i, qq, m);
+        const double* bq = lds + qq * P::PAD;
+        const double za = bq[padx(m)], zb = bq[padx(i == 0 && m == 0 ? L / 2 : L - m)];
+        if (c) {
+          Zm[i].y = za;
+          Zp[i].y = zb;
+        } else {
+          Zm[i].x = za;
+          Zp[i].x = zb;
+        }
+      }
+    }
+    double2* hb = Hout + __builtin_amdgcn_readfirstlane(y0);
+#pragma unroll
+    for (int i = 0; i < PAIRS; ++i) {
+      int qq, m;
+      pair(i, qq, m);
+      const bool z0 = i == 0 && m == 0;
+      const int mp = z0 ? L / 2 : L - m;
+      const double2 Zc = cconj(Zp[i]);
+      const double2 E = make_double2(0.5 * (Zm[i].x + Zc.x), 0.5 * (Zm[i].y + Zc.y));
+      const double2 D = csub(Zm[i], Zc);                      // = 2i O[m]
+      const double2 O = make_double2(0.5 * D.y, -0.5 * D.x);  // D / (2i)
+      const double2 WO = cmul(twN.w(m), O);
+      double2 o1 = cadd(E, WO);
+      double2 o2 = cconj(csub(E, WO));
+      if (z0) {  // slot 0 = X[0] + i X[L]; X[L/2] = conj(Z[L/2])
+        o1 = make_double2(Zm[i].x + Zm[i].y, Zm[i].x - Zm[i].y);
+        o2 = Zc;
+      }
+      hb[(unsigned)(m * M + qq)] = o1;
+      hb[(unsigned)(mp * M + qq)] = o2;
+    }
+  }
+}
+
 // Persistent grid: `per_cu` resident workgroups per CU (LDS-limited), a multiple of 8.
 static int persistent_grid(int ncu, int per_cu, int items) {
   int nb = ncu * per_cu;
@@ -929,6 +1089,36 @@ void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg
     case 2048: hipLaunchKernelGGL((col0_solve_kernel<2048>), dim3(1), dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
     case 4096: hipLaunchKernelGGL((col0_solve_kernel<4096>), dim3(1), dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
     default: hipLaunchKernelGGL((col0_solve_kernel<8192>), dim3(1), dim3(Plan<8192>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+  }
+  CFDJ_HIP(hipGetLastError());
+}
+
+bool rows_jac_supported(int nx, int rows) {
+  return CFDJ_ROWS_INV_NP > 0 && fused_rows_supported(nx, rows) && nx <= 4096;
+}
+
+template <int L>
+static void launch_rows_jac_t(const FusedPoissonArgs& a, double inv_np, hipStream_t st) {
+  constexpr int XR = 4 * Plan<L>::T <= 1024 ? 4 : 2;
+  const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
+  if (a.stream)
+    hipLaunchKernelGGL((rows_jac_np_kernel<L, XR, true>), grid, block, 0, st, a.H, a.f, a.C, a.rows,
+                       a.twL, a.twN, a.mmax, inv_np);
+  else
+    hipLaunchKernelGGL((rows_jac_np_kernel<L, XR, false>), grid, block, 0, st, a.H, a.f, a.C, a.rows,
+                       a.twL, a.twN, a.mmax, inv_np);
+}
+
+// a.H: the fourth field's scratch spectrum (columns 0..a.mmax), a.f: the three real fields,
+// a.C: the product's scratch spectrum (must not overlap a.H).
+void launch_rows_jac(const FusedPoissonArgs& a, double inv_np, hipStream_t st) {
+  if (!rows_jac_supported(a.nx, a.rows) || a.tile8 || a.mmax <= 0 || a.mmax > a.nx / 2 ||
+      a.H == nullptr || a.f == nullptr || a.C == nullptr || a.H == a.C)
+    throw Error{CFDJ_ERR_ARG, "fused product rows: unsupported arguments"};
+  switch (a.nx) {
+    case 1024: launch_rows_jac_t<512>(a, inv_np, st); break;
+    case 2048: launch_rows_jac_t<1024>(a, inv_np, st); break;
+    default: launch_rows_jac_t<2048>(a, inv_np, st); break;
   }
   CFDJ_HIP(hipGetLastError());
 }

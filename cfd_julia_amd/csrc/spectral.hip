@@ -650,6 +650,7 @@ struct cfdj_spec {
   // CFDJ_SPEC_PS32_HAND=0 keeps the library)
   bool hand32 = false;
   bool fuse32 = true;  // CFDJ_SPEC_PS32_FUSE=0: the product as a kernel of its own
+  bool fuse23 = false;  // the same for the 2/3 rule on the half spectrum (CFDJ_SPEC_PS23_FUSE=0)
   Real2d3Args a3{};
   Ps32HalfArgs s3{};
   double2 *tw3_l3 = nullptr, *tw3_l = nullptr, *tw3_n = nullptr, *tw3_m3 = nullptr;
@@ -709,6 +710,9 @@ struct cfdj_spec {
         product_real(gb, inv_np);
         CFDJ_HIP(hipGetLastError());
         launch_ps32_r2c2d3(a3, s3, Rj, J, jf, stream);
+        return;
+      } else if (fuse23) {
+        launch_half_ps23_jacobian(ha, wf, X, R, jf, stream);
         return;
       } else {
         launch_half_c2r2d(ha, kHalfPs23, wf, X, R, stream);
@@ -949,6 +953,9 @@ int cfdj_spec_create(int nx, int ny, double dx, double dy, double re, double eps
     h->half = want_hand && want_real && (h->px == nx || h->hand32) && half2d_supported(nx, ny) &&
               !(he && he[0] == '0');
     if (h->half) {
+      const char* f23 = std::getenv("CFDJ_SPEC_PS23_FUSE");
+      h->fuse23 = kind == CFDJ_SPEC_PS23 && half_ps23_jacobian_supported(nx) &&
+                  !(f23 && f23[0] == '0');
       h->fz.init(nx, ny);
       const int nxe = (2 * nx) / 3, nye = (2 * ny) / 3;
       h->ha = HalfSpecArgs{nx, h->fz.twL, h->fz.twN, h->fz.ncu, h->kx, nxe / 2, nye / 2,

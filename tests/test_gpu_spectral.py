@@ -366,3 +366,29 @@ def test_gpu_spectral_32_rule_hand_transforms_vs_library(spec, monkeypatch, n):
     if n == 1024:
         ref = so.jacobian_ps32(wf, so.wavespace(n, n, dx, dy), dx, dy)
         assert np.abs(out["hand"] - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+@pytest.mark.parametrize("n", [1024, 4096])
+def test_gpu_spectral_23_rule_fused_product_matches_unfused(spec, monkeypatch, n):
+    """pseudospectral_23_rule.jl:134-140 on the half-spectrum path: the fourth field's inverse
+    row pass, the product and its forward row pass as one kernel (default, grids of up to
+    4096^2) against the separate kernels (CFDJ_SPEC_PS23_FUSE=0): one Jacobian of the noisy
+    spectrum to 1e-12 of max|jf|, fields and spectra after 2 steps to 1e-12 of their maxima."""
+    dx, dy, _, _ = vo.vm_grid(n, n)
+    wf = _noisy_spectrum(n)
+    w0 = _noisy_start(n)
+    jac, out, spc = {}, {}, {}
+    for name, env in (("fused", None), ("unfused", "0")):
+        monkeypatch.delenv("CFDJ_SPEC_PS23_FUSE", raising=False)
+        if env is not None:
+            monkeypatch.setenv("CFDJ_SPEC_PS23_FUSE", env)
+        with spec.SpectralNS2D(n, n, dx, dy, 1000.0, "2/3") as h:
+            jac[name] = h.jacobian(wf)
+            h.upload_interior(w0)
+            h.step(2.5e-4, 2)
+            out[name] = h.download()
+            spc[name] = h.spectrum()
+    assert np.isfinite(out["fused"]).all()
+    assert np.abs(jac["fused"] - jac["unfused"]).max() <= 1e-12 * np.abs(jac["unfused"]).max()
+    assert np.abs(out["fused"] - out["unfused"]).max() <= 1e-12 * np.abs(out["unfused"]).max()
+    assert np.abs(spc["fused"] - spc["unfused"]).max() <= 1e-12 * np.abs(spc["unfused"]).max()
