@@ -1278,6 +1278,7 @@ struct cfdj_cavity {
   double2* spec = nullptr;
   // DST-I on the cavity's own interior (dst_poisson.hip; powers of two 512..4096)
   bool use_dst = false;
+  int dst_half = 0;  // passes on the half-length DST kernels (dst_half_passes)
   double2* dstT = nullptr;
   double2 *twX = nullptr, *twY = nullptr;
   int ncu = 256;
@@ -1317,6 +1318,7 @@ struct cfdj_cavity {
     a.ncu = ncu;
     a.sprev = nullptr;
     a.part = nullptr;
+    a.half = dst_half;
     return a;
   }
 
@@ -1419,7 +1421,7 @@ struct cfdj_cavity {
   void flush_rms() {
     if (rms_pending == 0) return;
     hipLaunchKernelGGL(sumsq_final_kernel, dim3(rms_pending), dim3(256), 0, stream, part,
-                       dst_rows_grid(nx, ny, ncu), (double)(nx + 1) * (ny + 1),
+                       dst_rows_grid(nx, ny, ncu, dst_half), (double)(nx + 1) * (ny + 1),
                        d_rms + rms_first, kParts);
     CFDJ_HIP(hipGetLastError());
     rms_pending = 0;
@@ -1530,6 +1532,7 @@ int cfdj_cavity_create(int nx, int ny, double dx, double dy, double re, int devi
     const char* ext_env = std::getenv("CFDJ_CAVITY_EXT");  // A/B: the extension-grid solver
     if (dst_poisson_supported(nx, ny) && !(ext_env && ext_env[0] == '1')) {
       h->use_dst = true;
+      h->dst_half = dst_half_passes(nx, ny);
       h->dstT = dalloc<double2>((size_t)(nx / 2) * ny);
       h->twX = twiddle_table(NX);
       h->twY = NY == NX ? h->twX : twiddle_table(NY);

@@ -256,12 +256,19 @@ struct DstPoissonArgs {
   const double2* twY;  // exp(-2 pi i k / (2ny))
   int ncu;
   // optional (pass 2): per-workgroup sums of (s - sprev)^2 over the interior into part[0 ..
-  // dst_rows_grid(nx, ny, ncu))
+  // dst_rows_grid(nx, ny, ncu, half))
   const double* sprev;
   double* part;
+  // passes on the half-length transform (bit p = pass p) instead of the odd extension's:
+  // dst_half_passes(nx, ny)
+  int half;
 };
 bool dst_poisson_supported(int nx, int ny);
-int dst_rows_grid(int nx, int ny, int ncu);
+// Which passes run the half-length DST kernels: they halve the arithmetic and the threads per
+// transform, which pays where a pass still fills the chip (row passes from nx = 4096, column
+// pass from ny = 2048); CFDJ_DST_HALF=0 / 1 (read at the call) forces none / all.
+int dst_half_passes(int nx, int ny);
+int dst_rows_grid(int nx, int ny, int ncu, int half);
 void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st);
 
 // In-place 2-D complex FFT of `batch` nx-by-ny arrays (x contiguous) in two passes,

@@ -24,6 +24,8 @@
 #pragma clang fp contract(fast)
 #include "fft_lds.hpp"
 
+#include <cstdlib>
+
 namespace cfdj {
 
 namespace {
@@ -464,6 +466,331 @@ __global__ __launch_bounds__((Plan<M2, kDstNV>::T))
     }
 }
 
+// ---------------------------------------------------------------------------------------
+// Half-length DST-I.  The kernels above transform the odd extension of a row: a complex FFT
+// of length 2n for two rows of n - 1 values.  The ones below get the same coefficients from a
+// complex FFT of length n (half the arithmetic, half the LDS): with y_0 = 0,
+//   y_j = sin(pi j / n) (x_j + x_{n-j}) + (x_j - x_{n-j}) / 2,   j = 1 .. n-1,
+// and Y = FFT_n(y) = R + i I, the sine coefficients S_k = 2 sum_j x_j sin(pi j k / n) are
+//   S_{2k} = -2 I_k,      S_{2k+1} = S_{2k-1} + 2 R_k   (S_1 = R_0),
+// i.e. the odd ones are a running sum over k.  Two rows a, b ride one complex transform
+// z = y_a + i y_b; their spectra separate by pairing Z_k with conj Z_{n-k}.  Round-off grows
+// with the running sum: 3-5e-15 of max|S| at n = 2048..4096 against scipy's DST-I (the
+// odd-extension route: 4e-16), far inside the 1e-12 the solve is held to.
+//
+// Z in natural order -> (S_a, S_b) at the even modes 2k (ev) and the odd modes 2k + 1 (od),
+// k = tid + T i, i < 8, of a team of T = N / 16 threads.  buf: the team's exchange buffer
+// (Plan<N>::PAD doubles); wtot: W = T / 64 double2 per team (unused where T <= 64).
+template <int N>
+__device__ __forceinline__ void dsth_post(double* buf, double2* wtot, const double2 (&v)[16],
+                                          int tid, double2 (&ev)[8], double2 (&od)[8]) {
+  using PL = Plan<N>;
+  constexpr int T = PL::T, SL = PL::NSTAGES - 1, W = T / 64 < 1 ? 1 : T / 64;
+  constexpr int WIDTH = T < 64 ? T : 64;
+  double2 zk[8], zm[8];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();
+    if (c) lds_write_half<N, SL, 1>(buf, v, tid);
+    else lds_write_half<N, SL, 0>(buf, v, tid);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = tid + T * i;
+      const double a = buf[padx(k)], b = buf[padx((N - k) & (N - 1))];
+      if (c) {
+        zk[i].y = a;
+        zm[i].y = b;
+      } else {
+        zk[i].x = a;
+        zm[i].x = b;
+      }
+    }
+  }
+  // Y_a = (Z_k + conj Z_{n-k}) / 2, Y_b = (Z_k - conj Z_{n-k}) / (2i)
+  double2 r[8];  // 2 R_k of rows a, b (k = 0: R_0)
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    ev[i] = make_double2(zm[i].y - zk[i].y, zk[i].x - zm[i].x);  // -2 I_k
+    r[i] = make_double2(zk[i].x + zm[i].x, zk[i].y + zm[i].y);
+    if (i == 0 && tid == 0) r[i] = make_double2(0.5 * r[i].x, 0.5 * r[i].y);
+  }
+  // running sum over k through the buffer: row a's terms at k, row b's at N/2 + k; a thread
+  // sums the 8 consecutive k of its chunk, the chunks' totals are scanned across the team
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    buf[padx(tid + T * i)] = r[i].x;
+    buf[padx(N / 2 + tid + T * i)] = r[i].y;
+  }
+  __syncthreads();
+  double2 c8[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    c8[j] = make_double2(buf[padx(8 * tid + j)], buf[padx(N / 2 + 8 * tid + j)]);
+#pragma unroll
+  for (int j = 1; j < 8; ++j) c8[j] = make_double2(c8[j].x + c8[j - 1].x, c8[j].y + c8[j - 1].y);
+  double2 tot = c8[7];  // inclusive scan of the chunk totals over the wavefront's team lanes
+  const int ln = tid & (WIDTH - 1);
+#pragma unroll
+  for (int d = 1; d < WIDTH; d <<= 1) {
+    const double tx = __shfl_up(tot.x, d, WIDTH), ty = __shfl_up(tot.y, d, WIDTH);
+    if (ln >= d) tot = make_double2(tot.x + tx, tot.y + ty);
+  }
+  double2 carry = make_double2(tot.x - c8[7].x, tot.y - c8[7].y);  // exclusive
+  if constexpr (W > 1) {
+    const int wv = tid / 64;
+    if (ln == 63) wtot[wv] = tot;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < W - 1; ++w)
+      if (w < wv) carry = make_double2(carry.x + wtot[w].x, carry.y + wtot[w].y);
+  }
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    buf[padx(8 * tid + j)] = c8[j].x + carry.x;
+    buf[padx(N / 2 + 8 * tid + j)] = c8[j].y + carry.y;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+    od[i] = make_double2(buf[padx(tid + T * i)], buf[padx(N / 2 + tid + T * i)]);
+}
+
+// W_N^e from the table of W_2N.
+template <int N>
+struct TwEven {
+  const double2* __restrict__ t;
+  __device__ __forceinline__ double2 w(int e) const { return t[2 * e]; }
+};
+
+// y of the definition above from x_p and x_{n-p}; sn = sin(pi p / n).
+__device__ __forceinline__ double dsth_y(double x1, double x2, double sn) {
+  return sn * (x1 + x2) + 0.5 * (x1 - x2);
+}
+
+template <int N>
+struct DsthCfg {
+  static constexpr int T = Plan<N>::T;
+  static constexpr int RP = 256 / T < 1 ? 1 : 256 / T;  // row pairs per workgroup
+  static constexpr int ROWS = 2 * RP;
+  static constexpr int THREADS = RP * T;
+  static constexpr int W = T / 64 < 1 ? 1 : T / 64;
+};
+
+// Forward row pass: rows ja, ja + 1 of the node array -> T[kappa][row] = (S_2kappa, S_2kappa+1).
+template <int N>
+__global__ __launch_bounds__(DsthCfg<N>::THREADS) void dsth_rows_fwd_kernel(
+    const double* __restrict__ w, int P, int ny, double2* __restrict__ Tt, int JT, double sgn,
+    const double2* __restrict__ tw2n) {
+  using PL = Plan<N>;
+  using C = DsthCfg<N>;
+  __shared__ double lds[C::RP * PL::PAD];
+  __shared__ double2 wtot[C::RP][C::W];
+  const TwEven<N> tw{tw2n};
+  const int q = threadIdx.x / C::T, tid = threadIdx.x % C::T;
+  double* buf = lds + q * PL::PAD;
+  const int slot0 = xcd_remap(blockIdx.x, gridDim.x) * C::ROWS;
+  const int ja = 1 + slot0 + 2 * q;
+  const bool oka = ja <= ny - 1, okb = ja + 1 <= ny - 1;
+  const double* ra = w + (size_t)(oka ? ja : 1) * P;
+  const double* rb = w + (size_t)(okb ? ja + 1 : 1) * P;
+  double2 v[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int p = tid + C::T * r;
+    const int p1 = p == 0 ? 1 : p, p2 = p == 0 ? 1 : N - p;  // (p = 0: y = 0)
+    const double sn = -tw2n[p].y;  // sin(pi p / N)
+    const double ya = dsth_y(ra[p1], ra[p2], sn), yb = dsth_y(rb[p1], rb[p2], sn);
+    v[r] = make_double2(p == 0 || !oka ? 0.0 : sgn * ya, p == 0 || !okb ? 0.0 : sgn * yb);
+  }
+  stage_regs<N, 0, -1>(v, tid, tw);
+  run_stages_half<N, 1, -1>(buf, v, tid, tw);
+  double2 ev[8], od[8];
+  dsth_post<N>(buf, wtot[q], v, tid, ev, od);
+  double2* tb = Tt + __builtin_amdgcn_readfirstlane(slot0);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const unsigned o = (unsigned)((tid + C::T * i) * JT + 2 * q);
+    tb[o] = make_double2(ev[i].x, od[i].x);
+    tb[o + 1] = make_double2(ev[i].y, od[i].y);
+  }
+}
+
+// Inverse row pass: T[kappa][row] -> rows ja, ja + 1 of s (interior nodes), and the partial
+// sums of (s_new - sprev)^2 as in dst_rows_inv_np_kernel.
+template <int N>
+__global__ __launch_bounds__(DsthCfg<N>::THREADS) void dsth_rows_inv_kernel(
+    const double2* __restrict__ Tt, int JT, double* __restrict__ s, int P, int ny,
+    const double2* __restrict__ tw2n, const double* __restrict__ sprev,
+    double* __restrict__ part) {
+  using PL = Plan<N>;
+  using C = DsthCfg<N>;
+  __shared__ double lds[C::RP * PL::PAD];
+  __shared__ double2 wtot[C::RP][C::W];
+  const TwEven<N> tw{tw2n};
+  const int q = threadIdx.x / C::T, tid = threadIdx.x % C::T;
+  double* buf = lds + q * PL::PAD;
+  const int slot0 = xcd_remap(blockIdx.x, gridDim.x) * C::ROWS;
+  const double2* tb = Tt + __builtin_amdgcn_readfirstlane(slot0);
+  double2 ea[8], eb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const unsigned o = (unsigned)((tid + C::T * i) * JT + 2 * q);
+    ea[i] = tb[o];
+    eb[i] = tb[o + 1];
+  }
+  if (tid == 0) ea[0].x = eb[0].x = 0.0;  // mode 0 of a sine series does not exist
+  // the rows' coefficients in natural order, one row at a time, read back at p and n - p
+  double2 v[16];
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = tid + C::T * i;
+      buf[padx(2 * k)] = c ? eb[i].x : ea[i].x;
+      buf[padx(2 * k + 1)] = c ? eb[i].y : ea[i].y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int p = tid + C::T * r;
+      const double y = dsth_y(buf[padx(p)], buf[padx((N - p) & (N - 1))], -tw2n[p].y);
+      if (c) v[r].y = y;
+      else v[r].x = y;
+    }
+  }
+  stage_regs<N, 0, -1>(v, tid, tw);
+  run_stages_half<N, 1, -1>(buf, v, tid, tw);
+  double2 ev[8], od[8];
+  dsth_post<N>(buf, wtot[q], v, tid, ev, od);
+  const int ja = 1 + slot0 + 2 * q;
+  const bool oka = ja <= ny - 1, okb = ja + 1 <= ny - 1;
+  double* sa = s + (size_t)ja * P;
+  double* sb = sa + P;
+  double acc = 0.0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = 2 * (tid + C::T * i);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (p + h >= 1) {
+        const double va = h ? od[i].x : ev[i].x, vb = h ? od[i].y : ev[i].y;
+        if (oka) sa[p + h] = va;
+        if (okb) sb[p + h] = vb;
+        if (sprev != nullptr) {
+          if (oka) {
+            const double d = va - sprev[(size_t)ja * P + p + h];
+            acc += d * d;
+          }
+          if (okb) {
+            const double d = vb - sprev[(size_t)(ja + 1) * P + p + h];
+            acc += d * d;
+          }
+        }
+      }
+    }
+  }
+  if (part != nullptr) {
+    __syncthreads();  // the buffer's last readers are done
+    double* red = lds;
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int off = C::THREADS / 2; off > 0; off >>= 1) {
+      if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+  }
+}
+
+// Column pass: one mode pair per workgroup (its column holds two real columns as the
+// components of a double2): y-DST, times iden, y-DST, in place.
+#ifndef CFDJ_DSTH_COLS_WAVES
+#define CFDJ_DSTH_COLS_WAVES 3
+#endif
+template <int N>
+__global__ __launch_bounds__((Plan<N>::T))
+    __attribute__((amdgpu_waves_per_eu(CFDJ_DSTH_COLS_WAVES, CFDJ_DSTH_COLS_WAVES))) void dsth_cols_kernel(
+        double2* __restrict__ Tt, int JT, const double* __restrict__ tx,
+        const double* __restrict__ ty, double scale, const double2* __restrict__ tw2n) {
+  using PL = Plan<N>;
+  constexpr int T = PL::T, W = T / 64 < 1 ? 1 : T / 64;
+  __shared__ double buf[PL::PAD];
+  __shared__ double2 wtot[W];
+  const TwEven<N> tw{tw2n};
+  const int tid = threadIdx.x;
+  const int kap = xcd_remap(blockIdx.x, gridDim.x);
+  double2* col = Tt + (size_t)kap * JT;  // row j in slot j - 1
+  double2 v[16];
+  {
+    // x_p into v, x_{n-p} into c2, y in place; p = 0 (thread 0's first element: y = 0) reads
+    // slot 0 for both, so its difference is zero like its sine
+    double2 c2[16];
+    const int z0 = tid == 0 ? 1 : 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = col[(unsigned)(tid + T * r - 1 + (r == 0 ? z0 : 0))];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      c2[r] = col[(unsigned)(N - 1 - tid - T * r - (r == 0 ? z0 * (N - 1) : 0))];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const double sn = -tw2n[tid + T * r].y;
+      v[r] = make_double2(dsth_y(v[r].x, c2[r].x, sn), dsth_y(v[r].y, c2[r].y, sn));
+    }
+  }
+  stage_regs<N, 0, -1>(v, tid, tw);
+  run_stages_half<N, 1, -1>(buf, v, tid, tw);
+  double2 ev[8], od[8];
+  dsth_post<N>(buf, wtot, v, tid, ev, od);
+  // times iden (lid_driven_cavity.jl:17) and the transforms' normalisation
+  const double txa = tx[2 * kap], txb = tx[2 * kap + 1];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int p = 2 * (tid + T * i);
+    const double t0 = ty[p], t1 = ty[p + 1];
+    const double2 e = ev[i], o = od[i];
+    ev[i] = p == 0 ? make_double2(0.0, 0.0)
+                   : make_double2((e.x * recip_nr(fd_symbol(txa, 1.0, t0))) * scale,
+                                  (e.y * recip_nr(fd_symbol(txb, 1.0, t0))) * scale);
+    od[i] = make_double2((o.x * recip_nr(fd_symbol(txa, 1.0, t1))) * scale,
+                         (o.y * recip_nr(fd_symbol(txb, 1.0, t1))) * scale);
+  }
+  // second transform: the products in natural order, one component at a time.  It works from
+  // an opaque copy of the thread index: the twiddles, sines and buffer addresses of the first
+  // transform are formed again instead of staying in registers (or spilled) across both.
+  int t2 = tid;
+  asm volatile("" : "+v"(t2));
+#pragma unroll
+  for (int c = 0; c < 2; ++c) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int k = t2 + T * i;
+      buf[padx(2 * k)] = c ? ev[i].y : ev[i].x;
+      buf[padx(2 * k + 1)] = c ? od[i].y : od[i].x;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int p = t2 + T * r;
+      const double y = dsth_y(buf[padx(p)], buf[padx((N - p) & (N - 1))], -tw2n[p].y);
+      if (c) v[r].y = y;
+      else v[r].x = y;
+    }
+  }
+  stage_regs<N, 0, -1>(v, t2, tw);
+  run_stages_half<N, 1, -1>(buf, v, t2, tw);
+  dsth_post<N>(buf, wtot, v, t2, ev, od);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const unsigned p = 2 * (t2 + T * i);
+    if (p >= 1) col[p - 1] = ev[i];
+    col[p] = od[i];
+  }
+}
+
 template <int M2>
 int dst_rows_grid_t(int ny, int ncu) {
   using C = DstRowCfg<M2>;
@@ -515,6 +842,24 @@ void launch_dst_cols(const DstPoissonArgs& a, hipStream_t st) {
 
 constexpr bool pow2(int n) { return n > 0 && (n & (n - 1)) == 0; }
 
+template <int N>
+void launch_dsth(int pass, const DstPoissonArgs& a, hipStream_t st) {
+  using C = DsthCfg<N>;
+  if (pass == 1) {
+    hipLaunchKernelGGL((dsth_cols_kernel<N>), dim3(a.nx / 2), dim3(Plan<N>::T), 0, st, a.T, a.JT,
+                       a.tx, a.ty, a.scale, a.twY);
+  } else if (pass == 0) {
+    hipLaunchKernelGGL((dsth_rows_fwd_kernel<N>), dim3(a.ny / C::ROWS), dim3(C::THREADS), 0, st,
+                       a.w, a.P, a.ny, a.T, a.JT, a.neg ? -1.0 : 1.0, a.twX);
+  } else {
+    hipLaunchKernelGGL((dsth_rows_inv_kernel<N>), dim3(a.ny / C::ROWS), dim3(C::THREADS), 0, st,
+                       a.T, a.JT, a.s, a.P, a.ny, a.twX, a.sprev, a.sprev ? a.part : nullptr);
+  }
+}
+
+template <int N>
+int dsth_rows_grid_t(int ny) { return ny / DsthCfg<N>::ROWS; }
+
 }  // namespace
 
 bool dst_poisson_supported(int nx, int ny) {
@@ -522,7 +867,22 @@ bool dst_poisson_supported(int nx, int ny) {
 }
 
 // Workgroups of the inverse row pass = entries of its `part` output (at most 2048).
-int dst_rows_grid(int nx, int ny, int ncu) {
+int dst_half_passes(int nx, int ny) {
+  const char* e = std::getenv("CFDJ_DST_HALF");
+  if (e && e[0] == '0') return 0;
+  if (e && e[0] == '1') return 7;
+  return (nx >= 4096 ? 1 | 4 : 0) | (ny >= 2048 ? 2 : 0);
+}
+
+int dst_rows_grid(int nx, int ny, int ncu, int half) {
+  if (half & 4) {
+    switch (nx) {
+      case 512: return dsth_rows_grid_t<512>(ny);
+      case 1024: return dsth_rows_grid_t<1024>(ny);
+      case 2048: return dsth_rows_grid_t<2048>(ny);
+      default: return dsth_rows_grid_t<4096>(ny);
+    }
+  }
   switch (2 * nx) {
     case 1024: return dst_rows_inv_grid_t<1024>(ny, ncu);
     case 2048: return dst_rows_inv_grid_t<2048>(ny, ncu);
@@ -535,6 +895,17 @@ void launch_dst_poisson_pass(int pass, const DstPoissonArgs& a, hipStream_t st) 
   if (!dst_poisson_supported(a.nx, a.ny) || a.JT < a.ny || a.P < a.nx + 1)
     throw Error{CFDJ_ERR_ARG, "DST Poisson: unsupported size"};
   const int n = pass == 1 ? a.ny : a.nx;
+  if (pass < 0 || pass > 2) throw Error{CFDJ_ERR_ARG, "DST Poisson: bad pass"};
+  if ((a.half >> pass) & 1) {
+    switch (n) {
+      case 512: launch_dsth<512>(pass, a, st); break;
+      case 1024: launch_dsth<1024>(pass, a, st); break;
+      case 2048: launch_dsth<2048>(pass, a, st); break;
+      default: launch_dsth<4096>(pass, a, st); break;
+    }
+    CFDJ_HIP(hipGetLastError());
+    return;
+  }
   switch (2 * n) {
     case 1024: pass == 1 ? launch_dst_cols<1024>(a, st) : launch_dst_rows<1024>(pass, a, st); break;
     case 2048: pass == 1 ? launch_dst_cols<2048>(a, st) : launch_dst_rows<2048>(pass, a, st); break;

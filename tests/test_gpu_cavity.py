@@ -299,3 +299,43 @@ def test_gpu_cavity_rhs_call_leaves_the_state_alone(lib):
     assert np.abs(wn - w_ref).max() < 1e-10 * max(1.0, np.abs(w_ref).max())
     assert np.abs(sn - s_ref).max() < 1e-12
     assert np.allclose(rms, rms_ref, rtol=1e-8, atol=1e-16)
+
+
+@pytest.mark.parametrize("half", ["0", "1"])
+@pytest.mark.parametrize("n", [512, 2048])
+def test_gpu_fps_sine_both_transform_routes(lib, monkeypatch, n, half):
+    """lid_driven_cavity.jl:11-21 by both routes to FFTW's RODFT00: the odd extension of a row
+    pair (a complex FFT of 2n points; CFDJ_DST_HALF=0) and the half-length transform (n points,
+    the odd coefficients as a running sum; CFDJ_DST_HALF=1).  The default picks per pass and
+    size; each alone must meet the oracle (scipy's DST-I) to 1e-12 of max|psi|."""
+    from cfd_julia_amd.cavity import fps_sine
+
+    monkeypatch.setenv("CFDJ_DST_HALF", half)
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    f = np.zeros((n + 1, n + 1), order="F")
+    rng = np.random.default_rng(n)
+    f[1:n, 1:n] = smooth_field(n - 1, n - 1, 4, 65) + 0.01 * rng.standard_normal((n - 1, n - 1))
+    s = fps_sine(n, n, dx, dy, f)
+    ref = co.fps_sine(f, dx, dy)
+    assert np.all(s[0, :] == 0) and np.all(s[:, 0] == 0) and np.all(s[n, :] == 0)
+    assert np.abs(s - ref).max() <= 1e-12 * np.abs(ref).max()
+
+
+def test_gpu_cavity_steps_half_length_transform(lib, monkeypatch):
+    """Cavity steps (512^2 x 3, the RMS partial sums of the inverse row pass included) on the
+    half-length DST kernels alone against the oracle, as test_gpu_cavity_steps_vs_oracle does
+    for the default mix."""
+    from cfd_julia_amd import cavity
+
+    monkeypatch.setenv("CFDJ_DST_HALF", "1")
+    n, nt = 512, 3
+    dt = 0.001 * (64 / n) ** 2
+    dx, dy, _, _ = co.cavity_grid(n, n)
+    wn = np.zeros((n + 1, n + 1), order="F")
+    sn = np.zeros((n + 1, n + 1), order="F")
+    rms = np.zeros(nt)
+    cavity.numerical(n, n, nt, dx, dy, dt, 100.0, wn, sn, rms)
+    w_ref, s_ref, rms_ref = co.cavity_numerical(n, n, nt, dt, 100.0)
+    assert np.abs(wn - w_ref).max() < 1e-10 * max(1.0, np.abs(w_ref).max())
+    assert np.abs(sn - s_ref).max() < 1e-12
+    assert np.allclose(rms, rms_ref, rtol=1e-8, atol=1e-16)
