@@ -27,20 +27,10 @@ namespace cfdj {
 
 namespace {
 
-// exp(-2 pi i j / 48), j < 16: the radix-3 step's twiddle of output k = tid + T3 j is that of
-// k = tid times this constant (T3 / L = 1/48); exp(-2 pi i j / 32), j < 8: the same for the
-// real-transform post-processing's W_N^m, m = m0 + TT j (TT / N = 1/32).  One table load per
-// thread instead of one per output.
-__device__ constexpr double kC48[16] = {
-    1.0, 0.99144486137381038, 0.96592582628906831, 0.92387953251128674,
-    0.86602540378443871, 0.79335334029123517, 0.70710678118654757, 0.60876142900872066,
-    0.5, 0.38268343236508984, 0.25881904510252074, 0.13052619222005171,
-    0.0, -0.1305261922200516, -0.25881904510252063, -0.3826834323650895};
-__device__ constexpr double kS48[16] = {
-    0.0, 0.13052619222005157, 0.25881904510252074, 0.38268343236508978,
-    0.5, 0.60876142900872066, 0.70710678118654746, 0.79335334029123517,
-    0.8660254037844386, 0.92387953251128674, 0.96592582628906831, 0.99144486137381038,
-    1.0, 0.99144486137381038, 0.96592582628906831, 0.92387953251128685};
+// exp(-2 pi i j / 32), j < 8: the real-transform post-processing's W_N^m of pair i is that of
+// pair 0 times this constant (m = m0 + TT i, TT / N = 1/32): one table load per thread instead
+// of one per pair.  (The radix-3 step's twiddles use exp(-2 pi i b / 16) of fft_lds.hpp the
+// same way.)
 __device__ constexpr double kC32[8] = {1.0, 0.98078528040323043, 0.92387953251128674,
                                        0.83146961230254524, 0.70710678118654757,
                                        0.55557023301960229, 0.38268343236508984,
@@ -398,12 +388,15 @@ template <int L3, int XR, bool NTS>
 __global__ __launch_bounds__((XR * Cfg3<L3>::TT)) CFDJ_ROWS3_INV_ATTR void rows3_inv_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M, int mmax,
     const double2* __restrict__ tw3, const double2* __restrict__ twL,
-    const double2* __restrict__ twN) {
+    const double2* __restrict__ twN, size_t hstride, size_t fstride) {
   using C = Cfg3<L3>;
   constexpr int L = C::L;
   __shared__ double lds[XR * C::PADL];
-  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3, tid = t % C::T3;
+  const int team = threadIdx.x / C::TT, t = threadIdx.x % C::TT, q = t / C::T3;
   const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  // blockIdx.y: the array of a batch (one launch for all of them: one tail instead of one each)
+  H += blockIdx.y * hstride;
+  f += blockIdx.y * fstride;
   double2 o[18];
   c2r_rows3<L3, XR>(H, M, mmax, y0, lds, threadIdx.x, tw3, twL, twN, o);
   // (a wave-uniform base and 32-bit element offsets: one offset register per access)
@@ -600,9 +593,11 @@ __global__ __launch_bounds__((XR * Cfg3<L3>::TT))
 
 template <int L3>
 void launch_rows3(bool fwd, const Real2d3Args& a, const double* fin, double* fout, double2* H,
-                  hipStream_t st) {
+                  hipStream_t st, int batch = 1) {
   constexpr int XR = CFDJ_ROWS3_XR;
-  const dim3 grid(a.n / XR), block(XR * Cfg3<L3>::TT);
+  // inverse: `batch` arrays, (mmax + 1) n complex / n n reals apart
+  const dim3 grid(a.n / XR, batch), block(XR * Cfg3<L3>::TT);
+  const size_t hs = (size_t)(a.mmax + 1) * a.n, fs = (size_t)a.n * a.n;
   if (fwd) {
     constexpr int XF = CFDJ_ROWS3_FWD_XR * Cfg3<L3>::TT <= 1024 ? CFDJ_ROWS3_FWD_XR : XR;
     const dim3 gridf(a.n / XF), blockf(XF * Cfg3<L3>::TT);
@@ -615,10 +610,10 @@ void launch_rows3(bool fwd, const Real2d3Args& a, const double* fin, double* fou
   } else {
     if (a.stream)
       hipLaunchKernelGGL((rows3_inv_kernel<L3, XR, true>), grid, block, 0, st, H, fout, a.n,
-                         a.mmax, a.tw3L, a.twL, a.twN);
+                         a.mmax, a.tw3L, a.twL, a.twN, hs, fs);
     else
       hipLaunchKernelGGL((rows3_inv_kernel<L3, XR, false>), grid, block, 0, st, H, fout, a.n,
-                         a.mmax, a.tw3L, a.twL, a.twN);
+                         a.mmax, a.tw3L, a.twL, a.twN, hs, fs);
   }
 }
 
@@ -670,21 +665,19 @@ bool real2d3_supported(int n) { return n == 1536 || n == 3072 || n == 6144; }
 
 void launch_c2r2d3(const Real2d3Args& a, double2* x, double* r, int batch, hipStream_t st) {
   check3(a);
-  const size_t half = (size_t)(a.mmax + 1) * a.n, full = (size_t)a.n * a.n;
   switch (a.n) {
     case 1536: launch_cols3<512>(false, a, x, batch, st); break;
     case 3072: launch_cols3<1024>(false, a, x, batch, st); break;
     default: launch_cols3<2048>(false, a, x, batch, st); break;
   }
   CFDJ_HIP(hipGetLastError());
-  for (int b = 0; b < batch; ++b) {
-    switch (a.n) {
-      case 1536: launch_rows3<256>(false, a, nullptr, r + b * full, x + b * half, st); break;
-      case 3072: launch_rows3<512>(false, a, nullptr, r + b * full, x + b * half, st); break;
-      default: launch_rows3<1024>(false, a, nullptr, r + b * full, x + b * half, st); break;
-    }
-    CFDJ_HIP(hipGetLastError());
+  if (batch < 1) return;
+  switch (a.n) {
+    case 1536: launch_rows3<256>(false, a, nullptr, r, x, st, batch); break;
+    case 3072: launch_rows3<512>(false, a, nullptr, r, x, st, batch); break;
+    default: launch_rows3<1024>(false, a, nullptr, r, x, st, batch); break;
   }
+  CFDJ_HIP(hipGetLastError());
 }
 
 void launch_r2c2d3(const Real2d3Args& a, const double* r, double2* x, hipStream_t st) {
@@ -716,21 +709,19 @@ void launch_ps32_c2r2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const doubl
                         double* r, int nrow, hipStream_t st) {
   check_ps32(a);
   if (nrow < 0 || nrow > 4) throw Error{CFDJ_ERR_ARG, "3/2-rule transform: bad array count"};
-  const size_t half = (size_t)(a.mmax + 1) * a.n, full = (size_t)a.n * a.n;
   switch (a.n) {
     case 1536: launch_cols3_ps32<512>(false, a, s, hs, x, st); break;
     case 3072: launch_cols3_ps32<1024>(false, a, s, hs, x, st); break;
     default: launch_cols3_ps32<2048>(false, a, s, hs, x, st); break;
   }
   CFDJ_HIP(hipGetLastError());
-  for (int b = 0; b < nrow; ++b) {
-    switch (a.n) {
-      case 1536: launch_rows3<256>(false, a, nullptr, r + b * full, x + b * half, st); break;
-      case 3072: launch_rows3<512>(false, a, nullptr, r + b * full, x + b * half, st); break;
-      default: launch_rows3<1024>(false, a, nullptr, r + b * full, x + b * half, st); break;
-    }
-    CFDJ_HIP(hipGetLastError());
+  if (nrow < 1) return;
+  switch (a.n) {
+    case 1536: launch_rows3<256>(false, a, nullptr, r, x, st, nrow); break;
+    case 3072: launch_rows3<512>(false, a, nullptr, r, x, st, nrow); break;
+    default: launch_rows3<1024>(false, a, nullptr, r, x, st, nrow); break;
   }
+  CFDJ_HIP(hipGetLastError());
 }
 
 void launch_ps32_r2c2d3(const Real2d3Args& a, const Ps32HalfArgs& s, const double* r, double2* x,
