@@ -358,6 +358,24 @@ class Job:
                 "tolerance": 1e-10}
 
 
+def parity_with_fallback(run_parity, environ=os.environ):
+    """The multi-rank field check with the default schedule of the y-slab step (halo exchanges
+    on a side stream, overlapped with the Poisson passes and the interior rows) and, if that
+    one does not meet the tolerance, once more with everything on one stream
+    (CFDJ_NO_OVERLAP=1, read by every handle created afterwards: the ladders then run that
+    schedule too).  `run_parity` returns the same dictionary on every rank (its error is the
+    maximum over ranks), so all ranks take the same branch."""
+    first = run_parity()
+    first["schedule"] = "side-stream overlap"
+    if first["linf_rel"] < first["tolerance"]:
+        return first
+    environ["CFDJ_NO_OVERLAP"] = "1"
+    second = run_parity()
+    second["schedule"] = "single stream (CFDJ_NO_OVERLAP=1)"
+    second["first_try"] = {"schedule": first["schedule"], "linf_rel": first["linf_rel"]}
+    return second
+
+
 def main(argv=None):
     argv = sys.argv[1:] if argv is None else argv
     ap = argparse.ArgumentParser()
@@ -439,7 +457,7 @@ def main(argv=None):
                 "note": "single-GPU path, measured on the ranks' own GPUs in this invocation "
                         "(max over ranks)"}
         if not args.no_parity:
-            parity = job.multi_rank_parity(nx, ny)
+            parity = parity_with_fallback(lambda: job.multi_rank_parity(nx, ny))
 
     h = job.handle(nx, ny, kind)
     h.set_poisson(args.poisson)
