@@ -358,6 +358,39 @@ class Job:
                 "tolerance": 1e-10}
 
 
+class Watchdog:
+    """A rank of a multi-GPU run that makes no progress for `seconds` (a collective whose peer
+    never arrives leaves the host blocked inside the library, where no exception can reach)
+    writes one JSON line naming the phase it was in and leaves the process with status 3, so a
+    hang costs the run its limit instead of the caller's.  `touch(phase)` restarts the clock."""
+
+    def __init__(self, seconds, write, leave=os._exit):
+        import threading
+
+        self.seconds, self.write, self.leave = seconds, write, leave
+        self.phase, self.timer, self.threading = "start", None, threading
+        self.touch("start")
+
+    def touch(self, phase):
+        self.phase = phase
+        if self.timer is not None:
+            self.timer.cancel()
+        if self.seconds > 0:
+            self.timer = self.threading.Timer(self.seconds, self.expire)
+            self.timer.daemon = True
+            self.timer.start()
+
+    def expire(self):
+        self.write({"error": f"no progress for {self.seconds} s in phase '{self.phase}'",
+                    "phase": self.phase})
+        self.leave(3)
+
+    def stop(self):
+        if self.timer is not None:
+            self.timer.cancel()
+            self.timer = None
+
+
 def parity_with_fallback(run_parity, environ=os.environ):
     """The multi-rank field check with the default schedule of the y-slab step (halo exchanges
     on a side stream, overlapped with the Poisson passes and the interior rows) and, if that
@@ -406,6 +439,9 @@ def main(argv=None):
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true",
                     help="do not record per-kernel HIP events in the timed region")
+    ap.add_argument("--watchdog", type=float, default=300.0, metavar="SECONDS",
+                    help="multi-GPU runs: give up (status 3, one JSON error line) when a phase "
+                         "makes no progress for this long; 0 = never")
     args = ap.parse_args(argv)
     if args.gpus < 1 or args.steps < 1:
         raise SystemExit("--gpus and --steps must be >= 1")
@@ -422,6 +458,16 @@ def main(argv=None):
     json_fd = os.dup(1)
     sys.stdout.flush()
     os.dup2(2, 1)
+    rank_env = int(os.environ.get("RANK", "0"))
+
+    def watchdog_line(d):
+        d = dict(d, rank=rank_env, n_gpus=args.gpus)
+        sys.stderr.write(f"bench.py watchdog: {d}\n")
+        sys.stderr.flush()
+        if rank_env == 0:
+            os.write(json_fd, (json.dumps(d) + "\n").encode())
+
+    dog = Watchdog(args.watchdog if world > 1 else 0.0, watchdog_line)
 
     # torch first: its HIP runtime must be the one in the process before libcfdj.so loads
     import torch  # noqa: F401
@@ -445,6 +491,7 @@ def main(argv=None):
         # (every rank runs it on its own GPU at the same time; rank 0's figure is used)
         ladders = {}
         if not args.no_ladders:
+            dog.touch("single-GPU reference 4096x4096")
             h1 = job.handle(4096, 4096, "single")
             try:
                 m1 = job.measure(h1, 4096, 4096, instrumented=False)
@@ -457,8 +504,10 @@ def main(argv=None):
                 "note": "single-GPU path, measured on the ranks' own GPUs in this invocation "
                         "(max over ranks)"}
         if not args.no_parity:
+            dog.touch(f"multi-rank parity {nx}x{ny}")
             parity = parity_with_fallback(lambda: job.multi_rank_parity(nx, ny))
 
+    dog.touch(f"headline {nx}x{ny}")
     h = job.handle(nx, ny, kind)
     h.set_poisson(args.poisson)
     if args.rows_per_wave:
@@ -593,6 +642,7 @@ def main(argv=None):
                 if (gx, gy) == (nx, ny) and args.poisson == "auto" and not args.rows_per_wave:
                     entry = dict(head)
                 else:
+                    dog.touch(f"ladder {key} {gx}x{gy}")
                     entry = job.case(gx, gy, "dist")
                 entry["efficiency_vs_n1"] = round(
                     entry["mlups"] / (n_gpus * ladders["n1_reference"]["mlups"]), 4)
@@ -608,6 +658,7 @@ def main(argv=None):
         workers = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
                       or os.cpu_count() or 1)
         line["cpu_baseline"] = cpu_baseline(nx, ny, args.cpu_steps, workers, warmup=1)
+    dog.stop()
     if rank == 0:
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(line) + "\n").encode())

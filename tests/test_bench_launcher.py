@@ -109,3 +109,28 @@ def test_parity_falls_back_to_the_single_stream_schedule():
     results = iter([{"linf_rel": float("nan"), "tolerance": 1e-10}, {"linf_rel": 1.0, "tolerance": 1e-10}])
     bad = bench.parity_with_fallback(lambda: next(results), env2)
     assert env2 == {"CFDJ_NO_OVERLAP": "1"} and bad["linf_rel"] == 1.0
+
+
+def test_watchdog_reports_the_stalled_phase():
+    """bench.Watchdog: no progress for its limit -> one error line naming the phase, status 3;
+    touch() restarts the clock, stop() disarms it, a limit of 0 never fires."""
+    import time
+
+    import bench
+
+    lines, codes = [], []
+    dog = bench.Watchdog(0.2, lines.append, codes.append)
+    dog.touch("headline 8192x8192")
+    time.sleep(0.1)
+    dog.touch("ladder weak")
+    time.sleep(0.1)
+    assert not lines and not codes  # touched in time
+    time.sleep(0.3)
+    assert codes == [3] and lines[0]["phase"] == "ladder weak" and "no progress" in lines[0]["error"]
+    lines.clear(), codes.clear()
+    dog = bench.Watchdog(0.1, lines.append, codes.append)
+    dog.stop()
+    never = bench.Watchdog(0.0, lines.append, codes.append)
+    never.touch("anything")
+    time.sleep(0.3)
+    assert not lines and not codes
