@@ -344,10 +344,10 @@ def test_gpu_spectral_jacobian_of_a_non_hermitian_spectrum(spec):
         assert np.abs(got - ref).max() <= 1e-12 * np.abs(ref).max(), n
 
 
-@pytest.mark.parametrize("n", [1024, 4096])
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
 def test_gpu_spectral_32_rule_hand_transforms_vs_library(spec, monkeypatch, n):
-    """pseudospectral_32_rule.jl:94-186 on product grids of 3 * 2^k points (1536, 6144 = 1.5 x
-    the benchmarked 4096): the hand-written radix-3 + power-of-two transforms on the columns
+    """pseudospectral_32_rule.jl:94-186 on product grids of 3 * 2^k points (1536, 3072, 6144 = 1.5
+    x the benchmarked 4096): the hand-written radix-3 + power-of-two transforms on the columns
     0..nx/2 of the padded half spectrum (fft2d_r2c3.hip) against the library's real transforms
     (CFDJ_SPEC_PS32_HAND=0) on a field with content in every mode: one Jacobian to 1e-12 of
     max|jf|, and at 1024 also against the oracle."""
@@ -368,7 +368,7 @@ def test_gpu_spectral_32_rule_hand_transforms_vs_library(spec, monkeypatch, n):
         assert np.abs(out["hand"] - ref).max() <= 1e-12 * np.abs(ref).max()
 
 
-@pytest.mark.parametrize("n", [1024, 4096])
+@pytest.mark.parametrize("n", [1024, 2048, 4096])
 def test_gpu_spectral_23_rule_fused_product_matches_unfused(spec, monkeypatch, n):
     """pseudospectral_23_rule.jl:134-140 on the half-spectrum path: the fourth field's inverse
     row pass, the product and its forward row pass as one kernel (default, grids of up to
