@@ -18,6 +18,10 @@
 //              are already the extended input), 1 / ((2nx)(2ny)) folded in.  In place.
 //   rows_inv : the second x-DST of each row pair from T, real rows out (interior only).
 //
+// The second half of this file holds the same three passes on a half-length transform (an
+// n-point FFT per row pair, the odd coefficients as a running sum), which dst_half_passes()
+// selects per pass where it is the faster one.
+//
 // Powers of two nx, ny in 512..4096 (FFT lengths 1024..8192); other sizes use the periodic
 // solver on the odd-odd extension (cavity.hip).  FMA contraction is on, as in the periodic
 // FFT passes: the transform is compared with scipy's DST-I at 1e-12 relative.

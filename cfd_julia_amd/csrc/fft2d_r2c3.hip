@@ -5,13 +5,17 @@
 //
 // A transform of length L = 3 L3 (L3 a power of two) is three independent length-L3 Stockham
 // transforms (the radix-16 plans of fft_lds.hpp) of the decimated inputs x[3 n + r], one per
-// third of the workgroup's team, followed by ONE decimation-in-time radix-3 step: X[k + q L3]
-// = F_0[k] + W_L^p F_1[k] + W_L^2p F_2[k], p = k + q L3.  The team's LDS buffer holds one
-// double per element (real and imaginary parts pass through it one after the other, as in
-// the column pass of the Poisson solver): it serves as the three sub-transforms' exchange
-// buffers, as the exchange of the radix-3 step (each thread reads the three F_r[k] of its 16
-// outputs and accumulates them component by component -- the step is linear), and as the
-// natural-order buffer of the (m, L - m) pairs of the real-transform pre/post-processing.
+// third of the workgroup's team, followed by the L3 radix-3 butterflies of a decimation-in-time
+// step: X[k + s L3] = F_0[k] + w3^s W_L^k F_1[k] + w3^2s W_L^2k F_2[k], s < 3.  The team's LDS
+// buffer holds one double per element (real and imaginary parts pass through it one after the
+// other, as in the column pass of the Poisson solver): it serves as the three sub-transforms'
+// exchange buffers, as the exchange of the radix-3 step (a thread reads the three F_r[k] of
+// each of its five or six butterflies), and as the natural-order buffer of the (m, L - m)
+// pairs of the real-transform pre/post-processing.
+//
+// The 3/2-rule solver's own kernels are here too: column passes that pad and form the
+// derivative spectra on load / unpad on store (cols3_ps32_*), and the row kernel that keeps
+// the fourth field and the product in the workgroup (rows3_jac_kernel).
 //
 // Layout of the half spectrum between the passes: column-major, element (m, y) at m n + y
 // (ky contiguous), columns m = 0 .. mmax only -- the padded spectrum is zero beyond the
