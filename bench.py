@@ -358,6 +358,10 @@ class Job:
                 "tolerance": 1e-10}
 
 
+FALLBACK_ENV = {"CFDJ_NO_OVERLAP": "1", "CFDJ_SLAB_W_HALO": "exchange",
+                "CFDJ_SLAB_PSI_HALO": "exchange"}
+
+
 class Watchdog:
     """A rank of a multi-GPU run that makes no progress for `seconds` (a collective whose peer
     never arrives leaves the host blocked inside the library, where no exception can reach)
@@ -392,19 +396,20 @@ class Watchdog:
 
 
 def parity_with_fallback(run_parity, environ=os.environ):
-    """The multi-rank field check with the default schedule of the y-slab step (halo exchanges
-    on a side stream, overlapped with the Poisson passes and the interior rows) and, if that
-    one does not meet the tolerance, once more with everything on one stream
-    (CFDJ_NO_OVERLAP=1, read by every handle created afterwards: the ladders then run that
-    schedule too).  `run_parity` returns the same dictionary on every rank (its error is the
-    maximum over ranks), so all ranks take the same branch."""
+    """The multi-rank field check with the default schedule of the y-slab step (substructured
+    path: one all-gather per solve carries everything, psi's halo rows are computed; other
+    paths: halo exchanges on a side stream) and, if that one does not meet the tolerance, once
+    more with the plainest schedule -- every halo row exchanged, on the one stream
+    (FALLBACK_ENV, read by every handle created afterwards: the ladders then run that schedule
+    too).  `run_parity` returns the same dictionary on every rank (its error is the maximum
+    over ranks), so all ranks take the same branch."""
     first = run_parity()
-    first["schedule"] = "side-stream overlap"
+    first["schedule"] = "default"
     if first["linf_rel"] < first["tolerance"]:
         return first
-    environ["CFDJ_NO_OVERLAP"] = "1"
+    environ.update(FALLBACK_ENV)
     second = run_parity()
-    second["schedule"] = "single stream (CFDJ_NO_OVERLAP=1)"
+    second["schedule"] = "fallback: " + " ".join(f"{k}={v}" for k, v in FALLBACK_ENV.items())
     second["first_try"] = {"schedule": first["schedule"], "linf_rel": first["linf_rel"]}
     return second
 

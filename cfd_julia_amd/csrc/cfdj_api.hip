@@ -110,6 +110,9 @@ struct Slab {
   bool cp_valid[3] = {false, false, false};
   double* cs8 = nullptr;
   double2* cs = nullptr;
+  // ... and psi-hat of the two rows just outside the slab (8-row tiled spectrum, rows 0 / 1),
+  // which the solve kernel leaves for the inverse row pass to turn into psi's halo rows
+  double2* hx8 = nullptr;
   void destroy() {
     dfree(wn);
     dfree(wa);
@@ -122,6 +125,7 @@ struct Slab {
     for (auto& c : colpart) dfree(c);
     dfree(cs8);
     dfree(cs);
+    dfree(hx8);
   }
 };
 
@@ -151,7 +155,9 @@ struct cfdj_vm {
   double2* TG = nullptr;
   int ncp = 0;  // column-sum partial rows (blocks of rows_per_wave rows)
   double2* G = nullptr;
-  size_t tg_block() const { return (size_t)4 * (nx / 2) + (size_t)rows; }
+  // (and the rank's first and last input rows, nx / 2 complex each: the neighbours' halo rows)
+  size_t tg_block() const { return (size_t)6 * (nx / 2) + (size_t)rows; }
+  size_t tg_rows_off() const { return (size_t)4 * (nx / 2) + (size_t)rows; }
   rocfft_plan g_fwd = nullptr, g_inv = nullptr;
   ncclComm_t comm = nullptr;
   // y-slabs: halo exchanges on a side stream, overlapped with the Poisson passes (omega
@@ -182,6 +188,35 @@ struct cfdj_vm {
   int g_steps = -1;
 
   bool slab_mode() const { return mode != Mode::Single; }
+  // Substructured path: psi's halo rows come out of the slab's own solve (the next slab's
+  // separator value and the operator's equation at this slab's separator row), so psi is not
+  // exchanged and the stage kernel runs as one launch.  CFDJ_SLAB_PSI_HALO=exchange at handle
+  // creation keeps the exchange.
+  bool local_psi = [] {
+    const char* e = std::getenv("CFDJ_SLAB_PSI_HALO");
+    return !(e && e[0] == 'e');
+  }();
+  bool psi_local() const {
+    return slab_mode() && use_schur && local_psi && fused_rows_take_col0(nx, rows);
+  }
+  // ... and omega's halo rows travel in the solve's all-gather: every rank's first and last
+  // input rows are part of its block, the stage kernel reads its neighbours' straight from the
+  // gather buffer.  With both, a stage has one collective and no exchange of its own, no side
+  // stream and no event.  CFDJ_SLAB_W_HALO=exchange keeps the omega exchange.
+  bool gather_w = [] {
+    const char* e = std::getenv("CFDJ_SLAB_W_HALO");
+    return !(e && e[0] == 'e');
+  }();
+  bool w_in_gather() const { return psi_local() && gather_w; }
+  // the slab whose block holds slab s's lower / upper halo row (a solo rehearsal has no
+  // neighbours: its own)
+  const double* gathered_row(const Slab& s, bool upper) const {
+    const int P = nranks;
+    int q = upper ? (s.rank + 1) % P : (s.rank + P - 1) % P;
+    if (slabs.size() == 1 && P > 1 && mode == Mode::Virtual) q = s.rank;
+    const double2* blk = TG + (size_t)q * tg_block() + tg_rows_off();
+    return reinterpret_cast<const double*>(upper ? blk : blk + nx / 2);
+  }
 
   // ---- timing -----------------------------------------------------------------------
   void reserve_events(size_t n) {
@@ -409,6 +444,7 @@ struct cfdj_vm {
       sa.tstride = blk;
       sa.tile8 = 1;
       sa.cs = s.cs;
+      sa.halo8 = psi_local() ? s.hx8 : nullptr;
       return sa;
     };
     // the slab's column sum per mode: the stage kernel's partials of this input (or a
@@ -440,6 +476,16 @@ struct cfdj_vm {
         a.back().col0 = G + slabs[i].row0;
         a.back().fx = slabs[i].cs8;
         a.back().Hx = slabs[i].cs;
+        if (w_in_gather())
+          a.back().wrows = TG + (size_t)slabs[i].rank * blk + tg_rows_off();
+        if (psi_local()) {  // pass 2 also writes psi's two halo rows
+          const Slab& sl = slabs[i];
+          a.back().hx_H = sl.hx8;
+          a.back().hx_lo = sl.ghost + 2 * (size_t)nx;
+          a.back().hx_hi = sl.ghost + 3 * (size_t)nx;
+          a.back().hx_c0lo = G + (sl.row0 + ny - 1) % ny;
+          a.back().hx_c0hi = G + (sl.row0 + sl.rows) % ny;
+        }
       }
     }
     for (size_t i = 0; i < a.size(); ++i) {
@@ -553,6 +599,10 @@ struct cfdj_vm {
     std::vector<const double*> src(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i)
       src[i] = st == 1 ? slabs[i].wn : st == 2 ? slabs[i].wa : slabs[i].wb;
+    if (psi_local()) {
+      stage_local_psi(st, dt, src);
+      return;
+    }
     if (slab_mode() && side && !timing && rows >= 3) {
       stage_overlapped(st, dt, src);
       return;
@@ -574,6 +624,40 @@ struct cfdj_vm {
         p.colpart = s.colpart[oi];
         s.cp_valid[oi] = true;
       }
+      launch_stage(st, p, stream);
+      tend();
+    }
+  }
+
+  // The y-slab stage of the substructured path: the omega halo exchange (on the side stream,
+  // during the Poisson passes, where there is one), the solve -- which leaves psi AND its two
+  // halo rows --, and the stage kernel over all rows in one launch.
+  void stage_local_psi(int st, double dt, const std::vector<const double*>& src) {
+    if (w_in_gather()) {
+      // (nothing: the rows ride in the solve's gather)
+    } else if (side && !timing) {
+      CFDJ_HIP(hipEventRecord(ev_src, stream));
+      CFDJ_HIP(hipStreamWaitEvent(side, ev_src, 0));
+      halo(false, src, side);
+      CFDJ_HIP(hipEventRecord(ev_whalo, side));
+      whalo_pending = true;
+    } else {
+      halo(false, src);
+    }
+    poisson(src, true);
+    comm_order();  // (a no-op where the Poisson path had a collective on the main stream)
+    for (size_t i = 0; i < slabs.size(); ++i) {
+      Slab& s = slabs[i];
+      double* out = st == 1 ? s.wa : st == 2 ? s.wb : s.wn;
+      tbegin(CFDJ_K_STAGE, st);
+      StageParams p = stage_params(s, src[i], s.wn, out, dt);
+      if (w_in_gather()) {
+        p.w_lo = gathered_row(s, false);
+        p.w_hi = gathered_row(s, true);
+      }
+      const int oi = st == 1 ? 1 : st == 2 ? 2 : 0;
+      p.colpart = s.colpart[oi];
+      s.cp_valid[oi] = true;
       launch_stage(st, p, stream);
       tend();
     }
@@ -771,7 +855,7 @@ struct cfdj_vm {
       rocfft_plan_description_destroy(desc);
       if (schur_ok(nx, ny, nranks)) {
         schur.init(nx, ny, dx, dy, eps, nranks);
-        TG = dalloc<double2>((size_t)nranks * ((size_t)4 * (nx / 2) + (size_t)(ny / nranks)));
+        TG = dalloc<double2>((size_t)nranks * ((size_t)6 * (nx / 2) + (size_t)(ny / nranks)));
         G = dalloc<double2>((size_t)ny);
         g_fwd = plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 1,
                           &len_y, 1, nullptr);
@@ -798,6 +882,8 @@ struct cfdj_vm {
       for (auto& s : slabs) {
         s.cs8 = dalloc<double>((size_t)8 * nx);
         s.cs = dalloc<double2>((size_t)8 * (nx / 2));
+        s.hx8 = dalloc<double2>((size_t)8 * (nx / 2));
+        CFDJ_HIP(hipMemset(s.hx8, 0, (size_t)8 * (nx / 2) * sizeof(double2)));
       }
       alloc_colparts();
     }
@@ -1051,11 +1137,10 @@ int cfdj_vm_create_virtual(int nx, int ny, double dx, double dy, double re, doub
     if (ov && ov[0] == '1') h->create_side();
     if (solo >= 0) {
       // what the absent ranks would have delivered: zeros (finite, so the step stays sane)
-      const size_t L = (size_t)nx / 2;
       auto zero = [](void* p, size_t bytes) {
         if (p) CFDJ_HIP(hipMemset(p, 0, bytes));
       };
-      zero(h->TG, (size_t)nranks * (4 * L + (size_t)h->rows) * sizeof(double2));
+      zero(h->TG, (size_t)nranks * h->tg_block() * sizeof(double2));
       zero(h->G, (size_t)ny * sizeof(double2));
       Slab& sl = h->slabs[0];
       zero(sl.X, (size_t)h->nxh * h->rows * sizeof(double2));

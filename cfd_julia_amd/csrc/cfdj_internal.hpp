@@ -224,7 +224,17 @@ struct FusedPoissonArgs {
                         // (instead of H's column 0) by pass 2; null: H only
   const double* fx;     // pass 0 with col0: one more workgroup transforms the first rows of
   double2* Hx;          // this 8-row array into this 8-row tiled spectrum (null: none)
+  double2* wrows;       // pass 0 with col0: the input's first and last rows, as they are, to
+                        // wrows[0 .. nx/2) and wrows[nx/2 .. nx) (null: none)
   int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
+  // pass 2 with col0 (8-mode tiles): two more rows -- rows 0 and 1 of the 8-row tiled spectrum
+  // hx_H (SchurArgs::halo8) -- go to the slab's halo rows hx_lo / hx_hi, their packed column 0
+  // from *hx_c0lo / *hx_c0hi (null: none)
+  const double2* hx_H;
+  double* hx_lo;
+  double* hx_hi;
+  const double2* hx_c0lo;
+  const double2* hx_c0hi;
   bool stream;          // pass 0: the input rows by streaming loads (load_stream)
   bool stream_out;      // pass 2 (small-item kernel): the output rows by streaming stores
 };
@@ -385,6 +395,11 @@ struct SchurArgs {
   const double* tA;     // [L] interface off-diagonal g(31)
   const double* tB;     // [L] interface diagonal -(2 + eps) + 2 g(1)
   const double* tiq;    // [L][K] inverse pivots of the K-1 interface system
+  const double* tD;     // [L] 2 + ep = -dy^2 d_m: the scaled operator's diagonal, negated
+  double2* halo8;       // optional: 8-row tiled spectrum receiving psi-hat of the rows just
+                        // outside the slab -- row 0: the row before the slab's first (from the
+                        // operator's equation at the separator row), row 1: the next slab's
+                        // separator row -- so psi's halo rows need no exchange
   double inv_dy2, dy2, out_scale, inv_ny;
   int rl, L, P, rank;
   int tile8;            // H in 8-mode tiles (sidx in poisson_fft.hip); required

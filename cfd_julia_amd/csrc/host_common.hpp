@@ -291,6 +291,10 @@ struct Fused {
     a.col0 = nullptr;
     a.fx = nullptr;
     a.Hx = nullptr;
+    a.wrows = nullptr;
+    a.hx_H = nullptr;
+    a.hx_lo = a.hx_hi = nullptr;
+    a.hx_c0lo = a.hx_c0hi = nullptr;
     a.stream = a.stream_out = stream_loads_pay((size_t)nx * rows * sizeof(double));
     return a;
   }
@@ -307,6 +311,7 @@ struct SchurTables {
   double inv_dy2 = 0, dy2 = 0;
   double *cinv = nullptr, *corr = nullptr, *g = nullptr;
   double *tip = nullptr, *tg = nullptr, *tA = nullptr, *tB = nullptr, *tiq = nullptr;
+  double* tD = nullptr;  // [L] 2 + ep: minus the diagonal of the operator scaled by dy^2
   int* jt = nullptr;  // [L/8] trace rows above round-off per tile
   bool ready() const { return cinv != nullptr; }
   void init(int nx, int ny, double dx, double dy, double eps, int nranks) {
@@ -326,7 +331,7 @@ struct SchurTables {
     std::vector<double> hc((size_t)L * P, 0.0), hr(L, 0.0);
     std::vector<double> hg((size_t)L * (rl + 1), 0.0);
     std::vector<double> hip((size_t)L * kC, 0.0), htg((size_t)L * (kC + 1), 0.0), hA(L, 0.0), hB(L, 1.0),
-        hiq((size_t)L * K, 0.0);
+        hiq((size_t)L * K, 0.0), hD(L, 0.0);
     std::vector<int> hjt(L / 8, 1);
     std::vector<ld> s2(rl), qk(rl + 1);
     for (int k = 0; k <= rl; ++k) {
@@ -390,6 +395,7 @@ struct SchurTables {
       const ld A = gc[kC - 1], B = -(2.0L + ep) + 2.0L * gc[1];
       hA[m] = (double)A;
       hB[m] = (double)B;
+      hD[m] = (double)(2.0L + ep);
       ld q = B;
       for (int k = 1; k < K; ++k) {
         if (k > 1) q = B - A * A / q;
@@ -404,6 +410,7 @@ struct SchurTables {
     tA = upload(hA);
     tB = upload(hB);
     tiq = upload(hiq);
+    tD = upload(hD);
     jt = dalloc<int>(hjt.size());
     CFDJ_HIP(hipMemcpy(jt, hjt.data(), hjt.size() * sizeof(int), hipMemcpyHostToDevice));
   }
@@ -413,7 +420,7 @@ struct SchurTables {
     return d;
   }
   void destroy() {
-    for (double** p : {&cinv, &corr, &g, &tip, &tg, &tA, &tB, &tiq}) dfree(*p);
+    for (double** p : {&cinv, &corr, &g, &tip, &tg, &tA, &tB, &tiq, &tD}) dfree(*p);
     dfree(jt);
   }
   SchurArgs args(double2* H, double2* T, int rank, double out_scale, int ny) const {
@@ -431,6 +438,8 @@ struct SchurTables {
     a.jt = jt;
     a.cs = nullptr;
     a.tiq = tiq;
+    a.tD = tD;
+    a.halo8 = nullptr;
     a.inv_dy2 = inv_dy2;
     a.dy2 = dy2;
     a.out_scale = out_scale;

@@ -581,12 +581,22 @@ constexpr int rows_np_xr() {
 // other arrays through them: stage kernels 87 -> 83 us, this pass 49 -> 47 (0.742 -> 0.727 ms
 // per step).  Chosen like the streaming loads: only where the fields outgrow the caches.
 // COL0 (y-slab path): the packed column 0 comes from the dense array col0[row] (where the
-// gathered column's solve leaves it) instead of the spectrum.
+// gathered column's solve leaves it) instead of the spectrum; and, where hx.H is set, the
+// workgroups beyond the slab's rows transform the first two rows of that 8-row tiled spectrum
+// (psi-hat of the rows just outside the slab, from the substructured solve) into the slab's
+// two halo rows hx.lo / hx.hi, their packed column 0 from hx.c0lo / hx.c0hi.
+struct HaloRows {
+  const double2* H;
+  double* lo;
+  double* hi;
+  const double2* c0lo;
+  const double2* c0hi;
+};
 template <int L, int XR, bool TILE, bool BAND = false, bool NTS = false, bool COL0 = false>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_, int mmax,
-    const double2* __restrict__ col0) {
+    const double2* __restrict__ col0, const HaloRows hx) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -594,7 +604,16 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
   const TwGlobal<2 * L> twN{twN_};
   const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
   double* buf = lds + q * P::PAD;
-  const int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  bool extra = false;
+  if constexpr (COL0) {
+    if (y0 >= M) {  // the blocks whose index the (bijective) remap puts beyond the rows
+      extra = true;
+      y0 -= M;
+      H = hx.H;
+      M = 8;
+    }
+  }
   const double2* base = H + sidx<TILE>(0, __builtin_amdgcn_readfirstlane(y0), M);
   double2 o1[PAIRS], o2[PAIRS];
   // pair i of the thread: row qq, columns m and L - m (16 consecutive lanes take 16
@@ -614,7 +633,7 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
     if (!BAND || m <= mmax) Xm = base[(unsigned)sidx<TILE>(m, qq, M)];
     if (!BAND || mq <= mmax) Xq = base[(unsigned)sidx<TILE>(mq, qq, M)];
     if constexpr (COL0)
-      if (z0) Xm = col0[y0 + qq];
+      if (z0) Xm = !extra ? col0[y0 + qq] : (y0 + qq == 0 ? *hx.c0lo : *hx.c0hi);
     const double2 Xp = cconj(Xq);
     const double2 S = cadd(Xm, Xp);
     const double2 D = cmul(cconj(twN.w(m)), csub(Xm, Xp));
@@ -646,6 +665,12 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
   constexpr int SL = P::NSTAGES - 1;
   constexpr int RL = P::radix(SL);
   double2* z = reinterpret_cast<double2*>(f + (size_t)(y0 + q) * (2 * L));
+  if constexpr (COL0) {
+    if (extra) {  // rows 0 and 1 of the extra spectrum are the halo rows; the rest is padding
+      if (y0 + q > 1) return;
+      z = reinterpret_cast<double2*>(y0 + q == 0 ? hx.lo : hx.hi);
+    }
+  }
 #pragma unroll
   for (int b = 0; b < 16 / RL; ++b)
 #pragma unroll
@@ -664,7 +689,8 @@ template <int L, int XR, bool TILE, bool NT, bool COL0 = false>
 __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_,
-    double2* __restrict__ col0, const double* __restrict__ fx, double2* __restrict__ Hx) {
+    double2* __restrict__ col0, const double* __restrict__ fx, double2* __restrict__ Hx,
+    double2* __restrict__ wrows) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -692,6 +718,17 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
 #pragma unroll
       for (int r = 0; r < R0; ++r)
         v[b * R0 + r] = load_stream<NT>(z + (unsigned)in_pos<L, 0>(tid, b, r));
+    // COL0 with wrows: the slab's first and last rows also go, as they are, to wrows[0 .. L)
+    // and wrows[L .. 2L) -- the neighbours' halo rows of this field, sent with the gather
+    if constexpr (COL0) {
+      if (wrows != nullptr && !extra && (y0 + q == 0 || y0 + q == M - 1)) {
+        double2* wr = wrows + (y0 + q == 0 ? 0 : L);
+#pragma unroll
+        for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+          for (int r = 0; r < R0; ++r) wr[in_pos<L, 0>(tid, b, r)] = v[b * R0 + r];
+      }
+    }
   }
   stage_regs<L, 0, -1>(v, tid, twL);
   run_stages_half<L, 1, -1>(buf, v, tid, twL);
@@ -942,21 +979,25 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
       if (a.rows % XR == 0) {
         const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
         if (pass == 0) {
-          if (a.fx && !(a.col0 && a.Hx))
+          if ((a.fx && !(a.col0 && a.Hx)) || (a.wrows && !a.col0))
             throw Error{CFDJ_ERR_ARG, "fused Poisson: extra row without dense column 0"};
           const dim3 gridx(a.rows / XR + (a.fx ? 1 : 0));
           auto fwd = [&](auto nt, auto c0) {
             hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, nt.value, c0.value>), gridx, block,
-                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0, a.fx, a.Hx);
+                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0, a.fx, a.Hx, a.wrows);
           };
           using T = std::true_type;
           using F = std::false_type;
           if (a.stream) a.col0 ? fwd(T{}, T{}) : fwd(T{}, F{});
           else a.col0 ? fwd(F{}, T{}) : fwd(F{}, F{});
         } else {
+          if (a.hx_H && !(a.col0 && a.hx_lo && a.hx_hi && a.hx_c0lo && a.hx_c0hi))
+            throw Error{CFDJ_ERR_ARG, "fused Poisson: halo rows without dense column 0"};
+          const HaloRows hx{a.hx_H, a.hx_lo, a.hx_hi, a.hx_c0lo, a.hx_c0hi};
+          const dim3 gridi(a.rows / XR + (a.hx_H ? (2 + XR - 1) / XR : 0));
           auto inv = [&](auto nts, auto c0) {
-            hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true, false, nts.value, c0.value>), grid,
-                               block, 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, a.col0);
+            hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, true, false, nts.value, c0.value>), gridi,
+                               block, 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, a.col0, hx);
           };
           using T = std::true_type;
           using F = std::false_type;
@@ -976,10 +1017,10 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
           const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
           if (a.stream)
             hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, false, true>), grid, block, 0, st, a.f,
-                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr);
+                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr, nullptr);
           else
             hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, false, false>), grid, block, 0, st, a.f,
-                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr);
+                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr, nullptr);
         } else {
           throw Error{CFDJ_ERR_ARG, "CFDJ_FWD_NP: workgroup too large for this row length"};
         }
@@ -994,13 +1035,15 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
         if (a.mmax > 0)  // (the spectral solvers' batches: plain stores measured as fast)
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false, true>), dim3(a.rows / XR),
                              dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN,
-                             a.mmax, nullptr);
+                             a.mmax, nullptr, HaloRows{});
         else if (a.stream_out)
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false, false, true>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, nullptr);
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, nullptr,
+                             HaloRows{});
         else
           hipLaunchKernelGGL((rows_inv_np_kernel<L, XR, false>), dim3(a.rows / XR),
-                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, nullptr);
+                             dim3(XR * Plan<L>::T), 0, st, a.H, a.s, a.rows, a.twL, a.twN, 0, nullptr,
+                             HaloRows{});
         return;
       }
     }

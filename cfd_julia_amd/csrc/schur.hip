@@ -253,6 +253,18 @@ __global__ __launch_bounds__(MW * K) void schur_solve_kernel(const SchurArgs a) 
   const double s = a.out_scale;
   const double2 v0 = V[k][mi], v1 = V[k + 1][mi];
   const double* g = sg[mi];
+  // psi-hat of the two rows just outside the slab: the next slab's separator value is known
+  // here (s_q), the previous slab's last row follows from the operator's equation at this
+  // slab's separator row, psi[-1] + psi[1] - (2 + ep) psi[0] = dy^2 f[0] (f[0] from the
+  // interface buffer, psi[1] formed here: nothing stays in registers for it)
+  if (a.halo8 != nullptr && k == 0) {
+    const double2 p1 = cadd(y[0], cadd(cscale(v0, g[1]), cscale(v1, g[C - 1])));
+    const double2 lo = csub(cadd(rint[0][mi], cscale(v0, a.tD[mm])), p1);
+    const double2 hi = V[K][mi];
+    double2* h8 = a.halo8 + (((size_t)tb * 8) << 3) + m8;  // row j at h8[8 j]
+    h8[0] = make_double2((lo.x + cst.x) * s, (lo.y + cst.y) * s);
+    h8[8] = make_double2((hi.x + cst.x) * s, (hi.y + cst.y) * s);
+  }
   tile[(size_t)(k * C) << 3] = make_double2((v0.x + cst.x) * s, (v0.y + cst.y) * s);
 #pragma unroll
   for (int i = 1; i < C; ++i) {

@@ -91,24 +91,25 @@ def test_gpus_2_without_two_gpus_exits_nonzero_with_the_reason():
 
 
 def test_parity_falls_back_to_the_single_stream_schedule():
-    """bench.parity_with_fallback: a multi-rank field check that fails under the side-stream
-    schedule is repeated with CFDJ_NO_OVERLAP=1 (which the handles created afterwards read);
-    a passing first check leaves the environment alone."""
+    """bench.parity_with_fallback: a multi-rank field check that fails under the default
+    schedule is repeated with the plainest one (bench.FALLBACK_ENV, which the handles created
+    afterwards read); a passing first check leaves the environment alone."""
     import bench
 
     env = {}
     ok = bench.parity_with_fallback(lambda: {"linf_rel": 3e-16, "tolerance": 1e-10}, env)
-    assert ok["schedule"] == "side-stream overlap" and "CFDJ_NO_OVERLAP" not in env
+    assert ok["schedule"] == "default" and not env
     results = iter([{"linf_rel": 2e-3, "tolerance": 1e-10}, {"linf_rel": 4e-16, "tolerance": 1e-10}])
     got = bench.parity_with_fallback(lambda: next(results), env)
-    assert env == {"CFDJ_NO_OVERLAP": "1"}
-    assert got["schedule"].startswith("single stream") and got["linf_rel"] == 4e-16
-    assert got["first_try"] == {"schedule": "side-stream overlap", "linf_rel": 2e-3}
+    assert env == {"CFDJ_NO_OVERLAP": "1", "CFDJ_SLAB_W_HALO": "exchange",
+                   "CFDJ_SLAB_PSI_HALO": "exchange"}
+    assert got["schedule"].startswith("fallback: CFDJ_NO_OVERLAP=1") and got["linf_rel"] == 4e-16
+    assert got["first_try"] == {"schedule": "default", "linf_rel": 2e-3}
     # not-a-number counts as a failure, and a second failure is reported as it is
     env2 = {}
     results = iter([{"linf_rel": float("nan"), "tolerance": 1e-10}, {"linf_rel": 1.0, "tolerance": 1e-10}])
     bad = bench.parity_with_fallback(lambda: next(results), env2)
-    assert env2 == {"CFDJ_NO_OVERLAP": "1"} and bad["linf_rel"] == 1.0
+    assert env2 == bench.FALLBACK_ENV and bad["linf_rel"] == 1.0
 
 
 def test_watchdog_reports_the_stalled_phase():

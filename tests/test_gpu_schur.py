@@ -126,10 +126,13 @@ def test_gpu_virtual_slabs_side_stream_schedule_is_bit_identical(cfdj, monkeypat
     staging buffer and reaches the shared arrays only through the side stream's copy, so a
     consumer that did not wait for its event would read the previous solve's values.  Several
     steps over several calls must equal the single-stream order bit for bit, and the oracle
-    to the north-star tolerance."""
+    to the north-star tolerance.  (The substructured path exchanges no halo rows by default:
+    the switches below put it back on the exchanging schedule this test is about.)"""
     dx, dy, x, y = vo.vm_grid(n, n)
     w0 = vo.vm_ic(n, n, x, y)
     dt = min(0.01, 5e-4 * (4096 / n) ** 2)
+    monkeypatch.setenv("CFDJ_SLAB_PSI_HALO", "exchange")
+    monkeypatch.setenv("CFDJ_SLAB_W_HALO", "exchange")
     out = {}
     for ov in ("0", "1"):
         monkeypatch.setenv("CFDJ_VIRTUAL_OVERLAP", ov)
@@ -144,3 +147,36 @@ def test_gpu_virtual_slabs_side_stream_schedule_is_bit_identical(cfdj, monkeypat
     if n <= 2048:
         ref = vo.numerical(w0, 3, dt, dx, dy, 1000.0)
         assert np.abs(out["1"] - ref).max() < 1e-10
+
+
+@pytest.mark.parametrize("n,P", [(2048, 4), (4096, 8), (4096, 2), (1024, 2)])
+def test_gpu_virtual_slabs_without_halo_exchange(cfdj, monkeypatch, n, P):
+    """The substructured y-slab step needs no halo exchange of its own: psi's two halo rows come
+    out of the slab's solve (the next slab's separator value; the previous slab's last row from
+    the operator's equation at this slab's separator row), omega's ride in the solve's
+    all-gather.  Against the exchanging schedules -- psi computed and omega exchanged
+    (CFDJ_SLAB_W_HALO=exchange), both exchanged (+ CFDJ_SLAB_PSI_HALO=exchange) -- after 3
+    steps: equal to round-off (1e-12 of max|w|; the computed psi rows differ from the
+    neighbour's own in the last bits), and the oracle to the north-star tolerance."""
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    dt = min(0.01, 5e-4 * (4096 / n) ** 2)
+    out = {}
+    for name, env in (("none", {}), ("omega", {"CFDJ_SLAB_W_HALO": "exchange"}),
+                      ("both", {"CFDJ_SLAB_W_HALO": "exchange", "CFDJ_SLAB_PSI_HALO": "exchange"})):
+        for k in ("CFDJ_SLAB_W_HALO", "CFDJ_SLAB_PSI_HALO"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+            assert h.poisson() == "schur"
+            h.upload_interior(w0)
+            h.step(dt, 2)
+            h.step(dt, 1)
+            out[name] = h.download_interior()
+    scale = np.abs(out["both"]).max()
+    assert np.array_equal(out["none"], out["omega"])  # the same rows, by another route
+    assert np.abs(out["none"] - out["both"]).max() <= 1e-12 * scale
+    if n <= 2048:
+        ref = vo.numerical(w0, 3, dt, dx, dy, 1000.0)
+        assert np.abs(out["none"] - ref).max() < 1e-10
