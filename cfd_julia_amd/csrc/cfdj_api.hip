@@ -937,8 +937,11 @@ cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int
   h->eps = eps;
   h->nranks = nranks;
   h->rank = rank;
-  // rows per wavefront: keep >= ~8 waves per CU at the benchmark sizes
-  h->rows_per_wave = ny / nranks >= 2048 ? 32 : 8;  // measured sweep: 32 best at 4096^2
+  // rows per wavefront of the marching stage kernel, from sweeps of the whole step: one GPU
+  // (grids the row-group kernel does not take) 32 from 2048 rows on; a y-slab 16 from 8 M
+  // cells on (8192 x 1024 .. 4096: 1-4 % better than 8 and 32; 4096 x 2048: 2 %), else 8
+  if (nranks == 1) h->rows_per_wave = ny >= 2048 ? 32 : 8;
+  else h->rows_per_wave = (long long)nx * (ny / nranks) >= (1LL << 23) ? 16 : 8;
   CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   if (mode == Mode::Virtual && solo_rank >= 0) {
     // one rank's share of the nranks-rank step, alone on this GPU: its slab only, every

@@ -437,6 +437,84 @@ __global__ __launch_bounds__((Plan<M>::T)) void col0_solve_kernel(
     for (int r = 0; r < RL; ++r) dst[out_pos<M, SL>(tid, b, r)] = v[b * RL + r];
 }
 
+// The same solve as two workgroups, one per real column (c = 0: the kx = eps column, the real
+// parts of the packed column; c = 1: kx = -pi, the imaginary parts): a real transform of
+// length M as a complex one of length H = M/2 on z[j] = x[2j] + i x[2j+1],
+//   X[k] = E + W_M^k O,  X[H-k] = conj(E - W_M^k O),
+//   E = (Z[k] + conj Z[H-k]) / 2,  O = (Z[k] - conj Z[H-k]) / (2i),
+// both divided by the column's own symbol, and back through
+//   Z'[k] = (Y[k] + conj Y[H-k]) + i conj(W_M^k) (Y[k] - conj Y[H-k]),
+// whose inverse transform of length H is y[2j] + i y[2j+1] of the length-M inverse.  Half
+// the transform length per workgroup, on two CUs: this kernel sits alone on every rank's
+// critical path between the all-gather and the row pass.
+template <int H>
+struct TwEvery2nd {  // W_H^e out of the table of W_2H
+  const double2* __restrict__ t;
+  __device__ __forceinline__ double2 w(int e) const { return t[2 * e]; }
+};
+#ifndef CFDJ_COL0_SPLIT
+#define CFDJ_COL0_SPLIT 1
+#endif
+template <int M>
+__global__ __launch_bounds__((Plan<M / 2>::T)) void col0_split_kernel(
+    const double2* __restrict__ src, size_t seg_stride, int rl_log2, double2* __restrict__ dst,
+    const double2* __restrict__ twM_, const DivArgs da) {
+  constexpr int H = M / 2;
+  using P = Plan<H>;
+  __shared__ double2 lds[P::PAD];
+  const TwEvery2nd<H> twH{twM_};
+  const int tid = threadIdx.x;
+  const int c = blockIdx.x;
+  const double sgn = da.neg ? -1.0 : 1.0;
+  double2 a[16];
+  constexpr int R0 = P::radix(0);
+#pragma unroll
+  for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+    for (int r = 0; r < R0; ++r) {
+      const int y = 2 * in_pos<H, 0>(tid, b, r);  // (y and y + 1 share a segment)
+      const double* e = reinterpret_cast<const double*>(
+          src + (size_t)(y >> rl_log2) * seg_stride + (y & ((1 << rl_log2) - 1)));
+      a[b * R0 + r] = make_double2(e[c], e[2 + c]);
+    }
+  col_fft<H, -1, false>(lds, a, tid, twH);
+  double2 v[16];
+  fwd_to_inv<H>(a, v);  // v[r] = Z[k], k = tid + T r
+  __syncthreads();       // the forward transform's last LDS reads
+#pragma unroll
+  for (int r = 0; r < 16; ++r) lds[padx(tid + P::T * r)] = v[r];
+  __syncthreads();
+  const double ax = fd_symbol_x(da.aa, da.bb, da.cx[c ? da.L : 0]);
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const int k = tid + P::T * r;
+    const double2 Zc = cconj(lds[padx((H - k) & (H - 1))]);
+    const double2 w = twM_[k];
+    const double2 E = make_double2(0.5 * (v[r].x + Zc.x), 0.5 * (v[r].y + Zc.y));
+    const double2 D = csub(v[r], Zc);
+    const double2 Q = cmul(w, make_double2(0.5 * D.y, -0.5 * D.x));
+    const double dk = fd_symbol(ax, da.cc, da.cy[k]);
+    const double dp = fd_symbol(ax, da.cc, da.cy[H - k]);
+    double2 Yk = sym_apply(cadd(E, Q), dk, dk, sgn, false);
+    const double2 Yp = sym_apply(csub(E, Q), dp, dp, sgn, false);  // conj Y[H-k]
+    if (c == 0 && k == 0) Yk = make_double2(0.0, 0.0);              // e[1,1] = 0 (Common.jl:118)
+    const double2 S = cadd(Yk, Yp), U = cmul(cconj(w), csub(Yk, Yp));
+    v[r] = make_double2((S.x - U.y) * da.scale, (S.y + U.x) * da.scale);
+  }
+  col_fft<H, 1, false>(lds, v, tid, twH);  // (its first LDS write is behind a barrier)
+  constexpr int SL = P::NSTAGES - 1;
+  constexpr int RL = P::radix(SL);
+  double* out = reinterpret_cast<double*>(dst) + c;
+#pragma unroll
+  for (int b = 0; b < 16 / RL; ++b)
+#pragma unroll
+    for (int r = 0; r < RL; ++r) {
+      const int j = out_pos<H, SL>(tid, b, r);
+      out[4 * j] = v[b * RL + r].x;
+      out[4 * j + 2] = v[b * RL + r].y;
+    }
+}
+
 // ---------------------------------------------------------------------------------------
 // Pass 3: rows, packed half spectrum -> real (c2r).
 // ---------------------------------------------------------------------------------------
@@ -1127,6 +1205,20 @@ void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg
   const DivArgs da{a.cx,  a.cy,  nullptr,           a.aa, a.bb, a.cc,       a.scale,
                    a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, 0, ilog2(rows), 0u};
   const int rl_log2 = ilog2(rows);
+  static const bool split = [] {
+    const char* e = std::getenv("CFDJ_COL0_SPLIT");
+    return e ? e[0] != '0' : CFDJ_COL0_SPLIT != 0;
+  }();
+  if (split && rows >= 2) {
+    switch (a.ny) {
+      case 1024: hipLaunchKernelGGL((col0_split_kernel<1024>), dim3(2), dim3(Plan<512>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+      case 2048: hipLaunchKernelGGL((col0_split_kernel<2048>), dim3(2), dim3(Plan<1024>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+      case 4096: hipLaunchKernelGGL((col0_split_kernel<4096>), dim3(2), dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+      default: hipLaunchKernelGGL((col0_split_kernel<8192>), dim3(2), dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+    }
+    CFDJ_HIP(hipGetLastError());
+    return;
+  }
   switch (a.ny) {
     case 1024: hipLaunchKernelGGL((col0_solve_kernel<1024>), dim3(1), dim3(Plan<1024>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
     case 2048: hipLaunchKernelGGL((col0_solve_kernel<2048>), dim3(1), dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;

@@ -39,7 +39,12 @@ __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_dou
 // gL(0) = 1, gL(rl) = 0, tabulated on the host in long double, same tiling), so the
 // traces are two dot products over the slab column -- one streaming read, no transform.
 // Lane = (row r, mode mi): mi = tid % 8, rows j = 1 + tid/8, + 32, ...
-constexpr int kTraceThreads = 256;
+// (256 threads: with 1024 -- the slowest modes' whole-column tiles in one batch of loads --
+// the kernel measured 11.2 us against 8.9 at 8192 x 1024, 15.6 against 14.4 at 8192 x 2048)
+#ifndef CFDJ_TRACE_THREADS
+#define CFDJ_TRACE_THREADS 256
+#endif
+constexpr int kTraceThreads = CFDJ_TRACE_THREADS;
 __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurArgs a) {
   const int tb = xcd_remap(blockIdx.x, gridDim.x);  // tile: modes 8 tb .. 8 tb + 7
   const int mi = threadIdx.x & 7, r0 = threadIdx.x >> 3;

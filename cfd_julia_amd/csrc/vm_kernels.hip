@@ -18,6 +18,9 @@ namespace {
 #ifndef CFDJ_STAGE_WPB
 #define CFDJ_STAGE_WPB 4  // wavefronts per stage-kernel workgroup
 #endif
+#ifndef CFDJ_STAGE_WAVES_X
+#define CFDJ_STAGE_WAVES_X 0
+#endif
 constexpr int kWavesPerBlock = CFDJ_STAGE_WPB;
 constexpr int kColsPerWave = 2 * kWave;  // two x-adjacent points per lane (16-B loads)
 
@@ -39,7 +42,13 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
   // fastest, so x-neighbour strips and adjacent row chunks share one L2.
   const int strips = (nx + kColsPerWave - 1) / kColsPerWave;
   const int tile = xcd_remap(blockIdx.x, gridDim.x);
+#if CFDJ_STAGE_WAVES_X
+  // (variant: the workgroup's wavefronts side by side in x on the same rows)
+  const int sg = strips / kWavesPerBlock;
+  const int strip = (tile % sg) * kWavesPerBlock + wave, chunk = tile / sg;
+#else
   const int strip = tile % strips, chunk = tile / strips;
+#endif
   const int x = strip * kColsPerWave + 2 * lane;
   const bool valid = x < nx;
   const int xs = valid ? x : 0;
@@ -51,7 +60,11 @@ __global__ __launch_bounds__(64 * CFDJ_STAGE_WPB) void vm_stage_kernel(const Sta
   // A wavefront takes the part of ONE block of rows_per_wave rows (blocks are absolute: block
   // b = rows [b rpw, (b+1) rpw)) that lies in a window of the launch: the blocks the first
   // window touches, then those of the second.
+#if CFDJ_STAGE_WAVES_X
+  const int wi = chunk;
+#else
   const int wi = chunk * kWavesPerBlock + wave;
+#endif
   const int rpw = p.rows_per_wave;
   int blk, wy0, wy1;
   if (wi < p.nblk_a) {
@@ -410,9 +423,15 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   StageParams q = p;
   q.nblk_a = (p.y0 + p.ycount - 1) / rpw - p.y0 / rpw + 1;
   q.nblk_b = p.ycount_b > 0 ? (p.y0b + p.ycount_b - 1) / rpw - p.y0b / rpw + 1 : 0;
+#if CFDJ_STAGE_WAVES_X
+  if (strips % kWavesPerBlock != 0) throw Error{CFDJ_ERR_ARG, "stage kernel: nx % 512 != 0"};
+  const long chunks = q.nblk_a + q.nblk_b;
+  dim3 grid((unsigned)(strips / kWavesPerBlock * chunks));
+#else
   const long chunks = (q.nblk_a + q.nblk_b + kWavesPerBlock - 1) / kWavesPerBlock;
   if (strips * chunks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
   dim3 grid((unsigned)(strips * chunks));
+#endif
   dim3 block(kWave * kWavesPerBlock);
   switch (stage) {
     case 0: hipLaunchKernelGGL((vm_stage_kernel<0, false>), grid, block, 0, st, q); break;

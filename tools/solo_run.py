@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--ranks", type=int, default=8)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--rpw", type=int, default=0, help="rows per wavefront of the stage kernel")
     ap.add_argument("--all-slabs", action="store_true", help="every slab, not rank 0 alone")
     a = ap.parse_args()
     if not a.all_slabs:
@@ -38,6 +39,8 @@ def main():
     dt = 5e-4 * 2.0 * 4096.0 ** 2 / (nx * nx + ny * ny)
     with VortexMerger(nx, ny, dx, dy, 1000.0, kind="virtual", nranks=a.ranks) as h:
         row0, rows = h.slab()
+        if a.rpw:
+            h.set_rows_per_wave(a.rpw)
         x, y = dx * np.arange(nx + 1), dy * np.arange(ny + 1)
         wn = np.zeros((nx + 2, ny + 2), order="F")
         vm_ic(nx, rows - 1, x, y[row0:], wn[:, row0:])
@@ -47,7 +50,8 @@ def main():
         t0 = time.perf_counter()
         h.step(dt, a.steps)
         t = time.perf_counter() - t0
-        print(f"{nx}x{ny} rank 0 of {a.ranks} ({h.poisson()}): {t * 1e3 / a.steps:.4f} ms/step")
+        print(f"{nx}x{ny} rank 0 of {a.ranks} ({h.poisson()}) rpw {a.rpw or 'default'}: "
+              f"{t * 1e3 / a.steps:.4f} ms/step")
 
 
 if __name__ == "__main__":
