@@ -638,6 +638,9 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 // CFDJ_ROWS_INV_NP=0 builds without it (the persistent kernel everywhere).  The forward
 // pass keeps the persistent 4-row items: its column-segment WRITES would shrink to 32 B
 // with 2-row items, which measured slower (85 us in the step).
+#ifndef CFDJ_ROWS_INV_NP_CM_MAXL
+#define CFDJ_ROWS_INV_NP_CM_MAXL 2048  // column-major layout: longest half row it takes
+#endif
 #ifndef CFDJ_ROWS_INV_NP
 #define CFDJ_ROWS_INV_NP 1
 #endif
@@ -1107,7 +1110,7 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
       else if (xr == 4) go(std::integral_constant<int, 4>{});
       else go(std::integral_constant<int, 8>{});
       return;
-    } else if (pass != 0 && L <= 2048) {
+    } else if (pass != 0 && L <= CFDJ_ROWS_INV_NP_CM_MAXL) {
       constexpr int XR = rows_np_xr<L, false>();
       if (a.rows % XR == 0) {
         if (a.mmax > 0)  // (the spectral solvers' batches: plain stores measured as fast)
