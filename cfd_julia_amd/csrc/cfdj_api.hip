@@ -938,10 +938,16 @@ cfdj_vm* new_vm(int nx, int ny, double dx, double dy, double re, double eps, int
   h->nranks = nranks;
   h->rank = rank;
   // rows per wavefront of the marching stage kernel, from sweeps of the whole step: one GPU
-  // (grids the row-group kernel does not take) 32 from 2048 rows on; a y-slab 16 from 8 M
-  // cells on (8192 x 1024 .. 4096: 1-4 % better than 8 and 32; 4096 x 2048: 2 %), else 8
+  // (grids the row-group kernel does not take) 32 from 2048 rows on, else 8; a y-slab of 8 M
+  // cells and more 16 -- the tall-tile kernel's block, which the substructured path's slabs
+  // then run (8192^2 / 8: 45 us per launch against 50 for the marching kernel at its best
+  // setting) -- and 8 below (4096^2 / 4 and / 8: the marching kernel is 2 % ahead on the step)
   if (nranks == 1) h->rows_per_wave = ny >= 2048 ? 32 : 8;
   else h->rows_per_wave = (long long)nx * (ny / nranks) >= (1LL << 23) ? 16 : 8;
+  if (const char* e = std::getenv("CFDJ_SLAB_ROWS_PER_WAVE")) {  // (tests, A/B runs)
+    const int v = std::atoi(e);
+    if (nranks > 1 && v >= 1) h->rows_per_wave = v;
+  }
   CFDJ_HIP(hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking));
   if (mode == Mode::Virtual && solo_rank >= 0) {
     // one rank's share of the nranks-rank step, alone on this GPU: its slab only, every

@@ -9,6 +9,8 @@
 // Built with -ffp-contract=off: every expression is evaluated in the order the reference
 // writes it (no FMA contraction), so given the same streamfunction the stencil output is
 // bit-identical to the CPU oracle (oracle/vm_oracle.py: arakawa_rhs, rk3_step).
+#include <cstdlib>
+
 #include "stencil.hpp"
 
 namespace cfdj {
@@ -271,6 +273,123 @@ __global__ __launch_bounds__(256) CFDJ_TILE_ATTR void vm_stage_tile_kernel(const
   }
 }
 
+// Tall-tile variant, for the y-slabs of the substructured Poisson path: the row-group
+// kernel's access shape (workgroups in row-major order, so the chip works on one narrow band
+// of rows) that also delivers the slab's column sums.  A 256-thread workgroup owns 128
+// consecutive x of 16 consecutive rows, wavefront w the rows 4w .. 4w + 3 (two x per lane;
+// the wave's rows and their two halo rows loaded at once, the wave's two halo columns by one
+// load of lane i < 24 = (side, row, field) and shuffles).  The sixteen output rows meet in
+// LDS, where the first wavefront adds them up in the marching kernel's order (increasing, the
+// slab's row 0 last): the same partial sums bit for bit, one per 16-row block.
+#ifndef CFDJ_TALL_G
+#define CFDJ_TALL_G 4
+#endif
+constexpr int kTallG = CFDJ_TALL_G;        // rows per wavefront
+constexpr int kTallRows = 16;              // rows per workgroup = rows per column-sum block
+constexpr int kTallW = kTallRows / kTallG;  // wavefronts per workgroup
+#ifdef CFDJ_TALL_WAVES
+#define CFDJ_TALL_ATTR __attribute__((amdgpu_waves_per_eu(CFDJ_TALL_WAVES, CFDJ_TALL_WAVES)))
+#else
+#define CFDJ_TALL_ATTR
+#endif
+template <int STAGE, bool NT>
+__global__ __launch_bounds__(64 * kTallW) CFDJ_TALL_ATTR void vm_stage_tall_kernel(const StageParams p) {
+  constexpr int G = kTallG, NR = G + 2;
+  __shared__ double2 outs[kTallRows][kWave];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wave = threadIdx.x / kWave;
+  const int nx = p.nx, ny = p.ny;
+  const int strips = nx / kColsPerWave;
+  // workgroup b runs on XCD b % 8 = strip % 8: the blocks above and below share its L2
+  const int strip = blockIdx.x % strips, grp = blockIdx.x / strips;
+  const int x0 = strip * kColsPerWave;
+  const int x = x0 + 2 * lane;
+  const int yb = p.y0 + grp * kTallRows;
+  const int y0 = yb + wave * G;
+
+  double2 wv[NR], sv[NR], wnv[G];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    const double* wr = row_ptr(p.w, p.w_lo, p.w_hi, y0 - 1 + j, ny, nx);
+    const double* sr = row_ptr(p.s, p.s_lo, p.s_hi, y0 - 1 + j, ny, nx);
+    wv[j] = *reinterpret_cast<const double2*>(wr + x);
+    sv[j] = *reinterpret_cast<const double2*>(sr + x);
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    wnv[j] = make_double2(0.0, 0.0);
+    if constexpr (STAGE >= 2)
+      wnv[j] = load_stream<NT>(reinterpret_cast<const double2*>(p.wn + (size_t)(y0 + j) * nx + x));
+  }
+  static_assert(4 * NR <= kWave, "halo fetch needs one lane per value");
+  double halo = 0.0;
+  if (lane < 4 * NR) {
+    const int side = lane / (2 * NR), rem = lane % (2 * NR);
+    const int xh = side == 0 ? (x0 == 0 ? nx - 1 : x0 - 1)
+                             : (x0 + kColsPerWave >= nx ? x0 + kColsPerWave - nx
+                                                        : x0 + kColsPerWave);
+    const double* r = (rem & 1) ? row_ptr(p.s, p.s_lo, p.s_hi, y0 - 1 + rem / 2, ny, nx)
+                                : row_ptr(p.w, p.w_lo, p.w_hi, y0 - 1 + rem / 2, ny, nx);
+    halo = r[xh];
+  }
+  const StageCoef k = p.k;
+  Win ww[NR], sw[NR];
+#pragma unroll
+  for (int j = 0; j < NR; ++j) {
+    ww[j].a = wv[j].x;
+    ww[j].b = wv[j].y;
+    sw[j].a = sv[j].x;
+    sw[j].b = sv[j].y;
+    ww[j].l = __shfl_up(wv[j].y, 1, kWave);
+    ww[j].r = __shfl_down(wv[j].x, 1, kWave);
+    sw[j].l = __shfl_up(sv[j].y, 1, kWave);
+    sw[j].r = __shfl_down(sv[j].x, 1, kWave);
+    const double lw = __shfl(halo, 2 * j, kWave), ls = __shfl(halo, 2 * j + 1, kWave);
+    const double rw = __shfl(halo, 2 * NR + 2 * j, kWave);
+    const double rs = __shfl(halo, 2 * NR + 2 * j + 1, kWave);
+    if (lane == 0) {
+      ww[j].l = lw;
+      sw[j].l = ls;
+    }
+    if (lane == kWave - 1) {
+      ww[j].r = rw;
+      sw[j].r = rs;
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < G; ++j) {
+    double r0, r1;
+    pair_rhs(ww[j], ww[j + 1], ww[j + 2], sw[j], sw[j + 1], sw[j + 2], k, r0, r1);
+    double2 o;
+    o.x = stage_update<STAGE>(r0, ww[j + 1].a, wnv[j].x, k);
+    o.y = stage_update<STAGE>(r1, ww[j + 1].b, wnv[j].y, k);
+#ifdef CFDJ_TALL_PLAIN_STORE
+    *reinterpret_cast<double2*>(p.out + (size_t)(y0 + j) * nx + x) = o;
+#else
+    store_stream<NT>(reinterpret_cast<double2*>(p.out + (size_t)(y0 + j) * nx + x), o);
+#endif
+    outs[wave * G + j][lane] = o;
+  }
+  __syncthreads();
+  if (wave == 0) {
+    const bool hold = yb == 0;  // the slab's row 0 is added last
+    double2 c = make_double2(0.0, 0.0);
+#pragma unroll
+    for (int r = 0; r < kTallRows; ++r) {
+      if (r == 0 && hold) continue;
+      const double2 o = outs[r][lane];
+      c.x += o.x;
+      c.y += o.y;
+    }
+    if (hold) {
+      const double2 o = outs[0][lane];
+      c.x += o.x;
+      c.y += o.y;
+    }
+    *reinterpret_cast<double2*>(p.colpart + (size_t)(yb / kTallRows) * nx + x) = c;
+  }
+}
+
 // colpart[b][x] = sum over rows [b rpw, (b+1) rpw) of f[y][x], in the row order of the
 // stage kernel's csum (increasing, row 0 last), so a field gets the same partials either way.
 __global__ __launch_bounds__(256) void colpart_kernel(const double* __restrict__ f, int nx,
@@ -390,6 +509,19 @@ static bool stage_tile_ok(const StageParams& p) {
 
 bool stage_runs_row_group(const StageParams& p) { return stage_tile_ok(p); }
 
+// The tall-tile kernel where it applies: column partial sums wanted for whole 16-row blocks
+// in one launch (one window, nothing to add to), rows a multiple of 128.
+// CFDJ_STAGE_TALL=0: the marching kernel instead.
+static bool stage_tall_ok(const StageParams& p) {
+  static const bool on = [] {
+    const char* e = std::getenv("CFDJ_STAGE_TALL");
+    return !(e && e[0] == '0');
+  }();
+  return on && !p.march && p.colpart != nullptr && !p.cp_accumulate &&
+         p.rows_per_wave == kTallRows && p.nx % kColsPerWave == 0 && p.nx >= 8 * kColsPerWave &&
+         p.y0 % kTallRows == 0 && p.ycount % kTallRows == 0 && p.ycount > 0 && p.ycount_b == 0;
+}
+
 void launch_stage(int stage, const StageParams& p, hipStream_t st) {
   if (p.ycount <= 0 || p.y0 < 0 || p.y0 + p.ycount > p.ny)
     throw Error{CFDJ_ERR_ARG, "stage kernel: bad row window"};
@@ -411,6 +543,28 @@ void launch_stage(int stage, const StageParams& p, hipStream_t st) {
       default:
         if (p.stream) hipLaunchKernelGGL((vm_stage_tile_kernel<3, true>), grid, block, 0, st, p);
         else hipLaunchKernelGGL((vm_stage_tile_kernel<3, false>), grid, block, 0, st, p);
+        break;
+    }
+    CFDJ_HIP(hipGetLastError());
+    return;
+  }
+  if (stage_tall_ok(p)) {
+    const long blocks = (long)(p.nx / kColsPerWave) * (p.ycount / kTallRows);
+    if (blocks > 0x7fffffffL) throw Error{CFDJ_ERR_ARG, "grid too large"};
+    const dim3 grid((unsigned)blocks), block(64 * kTallW);
+    switch (stage) {
+      case 0: hipLaunchKernelGGL((vm_stage_tall_kernel<0, false>), grid, block, 0, st, p); break;
+      case 1:
+        if (p.stream) hipLaunchKernelGGL((vm_stage_tall_kernel<1, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((vm_stage_tall_kernel<1, false>), grid, block, 0, st, p);
+        break;
+      case 2:
+        if (p.stream) hipLaunchKernelGGL((vm_stage_tall_kernel<2, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((vm_stage_tall_kernel<2, false>), grid, block, 0, st, p);
+        break;
+      default:
+        if (p.stream) hipLaunchKernelGGL((vm_stage_tall_kernel<3, true>), grid, block, 0, st, p);
+        else hipLaunchKernelGGL((vm_stage_tall_kernel<3, false>), grid, block, 0, st, p);
         break;
     }
     CFDJ_HIP(hipGetLastError());

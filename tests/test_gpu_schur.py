@@ -180,3 +180,31 @@ def test_gpu_virtual_slabs_without_halo_exchange(cfdj, monkeypatch, n, P):
     if n <= 2048:
         ref = vo.numerical(w0, 3, dt, dx, dy, 1000.0)
         assert np.abs(out["none"] - ref).max() < 1e-10
+
+
+@pytest.mark.parametrize("n,P", [(1024, 2), (2048, 4), (4096, 8), (4096, 2)])
+def test_gpu_virtual_slabs_tall_tile_stage_kernel_matches_marching(cfdj, monkeypatch, n, P):
+    """Slabs of the substructured path whose column sums come in 16-row blocks (the default
+    from 8 M cells per slab on; here by CFDJ_SLAB_ROWS_PER_WAVE=16 at every size) run the
+    tall-tile stage kernel: 128 x 16-row workgroups in row-major order, a block's column sums
+    added up in LDS in the marching kernel's order.  Against the marching kernel with the same
+    blocks (set_rows_per_wave(16) selects it) the field after 3 steps -- 9 stage launches
+    whose column sums feed the next Poisson solve -- must be the same bits."""
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    dt = min(0.01, 5e-4 * (4096 / n) ** 2)
+    monkeypatch.setenv("CFDJ_SLAB_ROWS_PER_WAVE", "16")
+    out = {}
+    for name in ("tall", "marching"):
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+            assert h.poisson() == "schur"
+            if name == "marching":
+                h.set_rows_per_wave(16)
+            h.upload_interior(w0)
+            h.step(dt, 2)
+            h.step(dt, 1)
+            out[name] = h.download_interior()
+    assert np.array_equal(out["tall"], out["marching"])
+    if n <= 2048:
+        ref = vo.numerical(w0, 3, dt, dx, dy, 1000.0)
+        assert np.abs(out["tall"] - ref).max() < 1e-10
