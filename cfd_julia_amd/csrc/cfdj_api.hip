@@ -150,6 +150,8 @@ struct cfdj_vm {
   // substructured y-slab solve (schur.hip): traces of all ranks T, gathered column G
   SchurTables schur;
   bool use_schur = false;
+  double2* csT = nullptr;  // [nx/2] spectrum of the column sum over all ranks' rows
+  bool late_cs_on = true;  // CFDJ_SLAB_LATE_CS=0: a transform of the slab's own sums per rank
   // gather buffer of the substructured solve: per rank [4 L trace numbers][rows elements of
   // the packed column]; G: the solved packed column, dense
   double2* TG = nullptr;
@@ -208,6 +210,11 @@ struct cfdj_vm {
     return !(e && e[0] == 'e');
   }();
   bool w_in_gather() const { return psi_local() && gather_w; }
+  // the slab's column sums ride in the gather untransformed (see poisson_schur)
+  bool late_colsum() const {
+    return slab_mode() && use_schur && late_cs_on && fused_rows_take_colsum(nx, rows) &&
+           col0_solve_takes_colsum(nx, ny, rows);
+  }
   // the slab whose block holds slab s's lower / upper halo row (a solo rehearsal has no
   // neighbours: its own)
   const double* gathered_row(const Slab& s, bool upper) const {
@@ -437,31 +444,47 @@ struct cfdj_vm {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
     const bool col0_direct = fused_rows_take_col0(nx, rows);
+    // the slab's column sums (the constant-mode correction's input) travel untransformed: the
+    // forward row pass's extra workgroups add the partial rows up into the gather block, the
+    // packed column's solve adds the ranks' rows and transforms the total -- instead of a
+    // summing launch before the row pass and a transform per rank
+    const bool late_cs = late_colsum();
     const size_t blk = tg_block();
     auto col_piece = [&](const Slab& s) { return TG + (size_t)s.rank * blk + (size_t)4 * L; };
+    auto cs_piece = [&](const Slab& s) { return TG + (size_t)s.rank * blk + (size_t)3 * L; };
     auto schur_args = [&](const Slab& s) {
       SchurArgs sa = schur.args(s.X, TG, s.rank, out_scale, ny);
       sa.tstride = blk;
       sa.tile8 = 1;
       sa.cs = s.cs;
       sa.halo8 = psi_local() ? s.hx8 : nullptr;
+      if (late_cs) {
+        sa.tnum = 3;
+        sa.csT = csT;
+      }
       return sa;
     };
     // the slab's column sum per mode: the stage kernel's partials of this input (or a
     // colpart pass for other inputs), summed to one row, row r2c -> cs (8-mode tiles)
+    std::vector<int> cp_idx(slabs.size());
     for (size_t i = 0; i < slabs.size(); ++i) {
       Slab& s = slabs[i];
       const int idx = src[i] == s.wn ? 0 : src[i] == s.wa ? 1 : src[i] == s.wb ? 2 : 3;
+      cp_idx[i] = idx;
+      const bool fresh = idx == 3 || !s.cp_valid[idx];
+      if (late_cs && !fresh) continue;
       tbegin(CFDJ_K_FFT_FWD);
-      if (idx == 3 || !s.cp_valid[idx]) {
+      if (fresh) {
         launch_colpart(src[i], nx, rows, rows_per_wave, s.colpart[idx], stream);
         if (idx < 3) s.cp_valid[idx] = true;
       }
-      launch_colsum_row(s.colpart[idx], ncp, nx, s.cs8, stream);
-      if (!col0_direct) {  // (else: a workgroup of the slab's own row pass below)
-        FusedPoissonArgs ca = fused.args(sym, s.cs8, nullptr, s.cs, s.cs, 8, 0, 1, neg);
-        ca.tile8 = 1;
-        launch_fused_poisson_pass(0, ca, stream);
+      if (!late_cs) {
+        launch_colsum_row(s.colpart[idx], ncp, nx, s.cs8, stream);
+        if (!col0_direct) {  // (else: a workgroup of the slab's own row pass below)
+          FusedPoissonArgs ca = fused.args(sym, s.cs8, nullptr, s.cs, s.cs, 8, 0, 1, neg);
+          ca.tile8 = 1;
+          launch_fused_poisson_pass(0, ca, stream);
+        }
       }
       tend();
     }
@@ -474,8 +497,10 @@ struct cfdj_vm {
         // column m = 0 (packed DC / Nyquist): written straight into the rank's block of the
         // gather buffer by pass 0, read from the solved dense column G by pass 2
         a.back().col0 = G + slabs[i].row0;
-        a.back().fx = slabs[i].cs8;
-        a.back().Hx = slabs[i].cs;
+        if (!late_cs) {
+          a.back().fx = slabs[i].cs8;
+          a.back().Hx = slabs[i].cs;
+        }
         if (w_in_gather())
           a.back().wrows = TG + (size_t)slabs[i].rank * blk + tg_rows_off();
         if (psi_local()) {  // pass 2 also writes psi's two halo rows
@@ -491,6 +516,11 @@ struct cfdj_vm {
     for (size_t i = 0; i < a.size(); ++i) {
       FusedPoissonArgs a0 = a[i];
       if (col0_direct) a0.col0 = col_piece(slabs[i]);
+      if (late_cs) {
+        a0.cp = slabs[i].colpart[cp_idx[i]];
+        a0.ncp = ncp;
+        a0.csout = reinterpret_cast<double*>(cs_piece(slabs[i]));
+      }
       tbegin(CFDJ_K_FFT_FWD);
       launch_fused_poisson_pass(0, a0, stream);
       tend();
@@ -517,7 +547,11 @@ struct cfdj_vm {
     tbegin(CFDJ_K_DIVIDE);
     FusedPoissonArgs ga = fused.args(sym, nullptr, nullptr, G, G, ny, 0, 1, neg);
     if (col0_solve_supported(ny)) {
-      launch_col0_solve(ga, TG + (size_t)4 * L, blk, rows, G, stream);
+      if (late_cs)
+        launch_col0_solve(ga, TG + (size_t)4 * L, blk, rows, G, stream, TG + (size_t)3 * L, nranks,
+                          csT);
+      else
+        launch_col0_solve(ga, TG + (size_t)4 * L, blk, rows, G, stream);
     } else {
       for (int q = 0; q < nranks; ++q)
         launch_strided_copy(G + (size_t)q * rows, 1, TG + (size_t)q * blk + (size_t)4 * L, 1, rows,
@@ -857,6 +891,9 @@ struct cfdj_vm {
         schur.init(nx, ny, dx, dy, eps, nranks);
         TG = dalloc<double2>((size_t)nranks * ((size_t)6 * (nx / 2) + (size_t)(ny / nranks)));
         G = dalloc<double2>((size_t)ny);
+        csT = dalloc<double2>((size_t)nx / 2);
+        CFDJ_HIP(hipMemset(csT, 0, (size_t)(nx / 2) * sizeof(double2)));
+        if (const char* e = std::getenv("CFDJ_SLAB_LATE_CS")) late_cs_on = e[0] != '0';
         g_fwd = plans.add(rocfft_transform_type_complex_forward, rocfft_placement_inplace, 1,
                           &len_y, 1, nullptr);
         g_inv = plans.add(rocfft_transform_type_complex_inverse, rocfft_placement_inplace, 1,
@@ -899,6 +936,7 @@ struct cfdj_vm {
     schur.destroy();
     dfree(TG);
     dfree(G);
+    dfree(csT);
     dfree(spec);
     dfree(gather);
     dfree(d_flag);

@@ -226,6 +226,9 @@ struct FusedPoissonArgs {
   double2* Hx;          // this 8-row array into this 8-row tiled spectrum (null: none)
   double2* wrows;       // pass 0 with col0: the input's first and last rows, as they are, to
                         // wrows[0 .. nx/2) and wrows[nx/2 .. nx) (null: none)
+  const double* cp;     // pass 0 with col0: nx/64 more workgroups add the ncp partial rows
+  int ncp;              // cp[b][x] (a field's column sums per block of rows) up into
+  double* csout;        // csout[x] -- the launch that would do it otherwise (null: none)
   int mmax;             // pass 2, > 0: H is zero in the columns above mmax, which are not read
   // pass 2 with col0 (8-mode tiles): two more rows -- rows 0 and 1 of the 8-row tiled spectrum
   // hx_H (SchurArgs::halo8) -- go to the slab's halo rows hx_lo / hx_hi, their packed column 0
@@ -396,6 +399,9 @@ struct SchurArgs {
   const double* tB;     // [L] interface diagonal -(2 + eps) + 2 g(1)
   const double* tiq;    // [L][K] inverse pivots of the K-1 interface system
   const double* tD;     // [L] 2 + ep = -dy^2 d_m: the scaled operator's diagonal, negated
+  int tnum;             // numbers per mode in T: 4, or 3 (no column sum: csT has the total's)
+  const double2* csT;   // [L] spectrum of the column sum over ALL ranks' rows, or null: then
+                        // the solve adds up the ranks' fourth trace numbers
   double2* halo8;       // optional: 8-row tiled spectrum receiving psi-hat of the rows just
                         // outside the slab -- row 0: the row before the slab's first (from the
                         // operator's equation at the separator row), row 1: the next slab's
@@ -420,15 +426,22 @@ struct PackedDivParams {
 };
 void launch_packed_divide(const PackedDivParams& p, hipStream_t st);
 
-// The packed DC / Nyquist column of the y-slab path solved whole by ONE workgroup, everything
-// in LDS: the column's ny elements are read from P rank segments of `rows` elements (segment
-// q at src + q * seg_stride: the all-gather's receive layout), transformed along y, split into
-// the DC and the Nyquist column with the Z[k], Z[-k] symmetry, each divided by its reference
-// symbol (e[1,1] = 0), re-packed, transformed back and written to the dense column `dst`.
-// ny = 1024..8192 (a power of two); `a` supplies the symbol tables, the twiddles and `neg`.
+// The packed DC / Nyquist column of the y-slab path solved whole, everything in LDS (one
+// workgroup, or one per real column): the column's ny elements are read from P rank segments
+// of `rows` elements (segment q at src + q * seg_stride: the all-gather's receive layout),
+// transformed along y, split into the DC and the Nyquist column, each divided by its
+// reference symbol (e[1,1] = 0), re-packed, transformed back and written to the dense column
+// `dst`.  ny = 1024..8192 (a power of two); `a` supplies the symbol tables, the twiddles and
+// `neg`.  With cs_src (square grids, the two-workgroup form): one more workgroup adds up the P
+// ranks' column-sum rows (rank q's nx reals at cs_src + q * seg_stride) and writes the sum's
+// half spectrum, modes 1 .. nx/2 - 1, to csT.
 bool col0_solve_supported(int ny);
+bool col0_solve_takes_colsum(int nx, int ny, int rows);
 void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg_stride,
-                       int rows, double2* dst, hipStream_t st);
+                       int rows, double2* dst, hipStream_t st, const double2* cs_src = nullptr,
+                       int nranks = 0, double2* csT = nullptr);
+// Whether the forward row pass of the 8-mode-tile layout takes FusedPoissonArgs::cp.
+bool fused_rows_take_colsum(int nx, int rows);
 
 // Finiteness check: sets *flag = 1 if any element is not finite.
 void launch_check_finite(const double* a, size_t n, int* flag, hipStream_t st);

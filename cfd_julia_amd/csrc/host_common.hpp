@@ -292,6 +292,9 @@ struct Fused {
     a.fx = nullptr;
     a.Hx = nullptr;
     a.wrows = nullptr;
+    a.cp = nullptr;
+    a.ncp = 0;
+    a.csout = nullptr;
     a.hx_H = nullptr;
     a.hx_lo = a.hx_hi = nullptr;
     a.hx_c0lo = a.hx_c0hi = nullptr;
@@ -440,6 +443,8 @@ struct SchurTables {
     a.tiq = tiq;
     a.tD = tD;
     a.halo8 = nullptr;
+    a.tnum = 4;
+    a.csT = nullptr;
     a.inv_dy2 = inv_dy2;
     a.dy2 = dy2;
     a.out_scale = out_scale;

@@ -26,6 +26,7 @@
 #include <cstdlib>
 #include <type_traits>
 
+#include "colsum.hpp"
 #include "fft_lds.hpp"
 
 namespace cfdj {
@@ -458,7 +459,8 @@ struct TwEvery2nd {  // W_H^e out of the table of W_2H
 template <int M>
 __global__ __launch_bounds__((Plan<M / 2>::T)) void col0_split_kernel(
     const double2* __restrict__ src, size_t seg_stride, int rl_log2, double2* __restrict__ dst,
-    const double2* __restrict__ twM_, const DivArgs da) {
+    const double2* __restrict__ twM_, const DivArgs da, const double2* __restrict__ cs_src,
+    int cs_ranks, double2* __restrict__ csT) {
   constexpr int H = M / 2;
   using P = Plan<H>;
   __shared__ double2 lds[P::PAD];
@@ -468,6 +470,37 @@ __global__ __launch_bounds__((Plan<M / 2>::T)) void col0_split_kernel(
   const double sgn = da.neg ? -1.0 : 1.0;
   double2 a[16];
   constexpr int R0 = P::radix(0);
+  if (c == 2) {
+    // third workgroup (square grids: rows are as long as columns): the ranks' column-sum rows
+    // added up, rank 0 first, and the sum's half spectrum X[1 .. H-1] -- the same real
+    // transform, forward only
+#pragma unroll
+    for (int i = 0; i < 16; ++i) a[i] = make_double2(0.0, 0.0);
+#pragma unroll 1
+    for (int q = 0; q < cs_ranks; ++q) {
+      const double2* z = cs_src + (size_t)q * seg_stride;
+#pragma unroll
+      for (int b = 0; b < 16 / R0; ++b)
+#pragma unroll
+        for (int r = 0; r < R0; ++r) a[b * R0 + r] = cadd(a[b * R0 + r], z[in_pos<H, 0>(tid, b, r)]);
+    }
+    col_fft<H, -1, false>(lds, a, tid, twH);
+    double2 v[16];
+    fwd_to_inv<H>(a, v);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) lds[padx(tid + P::T * r)] = v[r];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = tid + P::T * r;
+      const double2 Zc = cconj(lds[padx((H - k) & (H - 1))]);
+      const double2 E = make_double2(0.5 * (v[r].x + Zc.x), 0.5 * (v[r].y + Zc.y));
+      const double2 D = csub(v[r], Zc);
+      csT[k] = cadd(E, cmul(twM_[k], make_double2(0.5 * D.y, -0.5 * D.x)));
+    }
+    return;
+  }
 #pragma unroll
   for (int b = 0; b < 16 / R0; ++b)
 #pragma unroll
@@ -771,7 +804,8 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_,
     double2* __restrict__ col0, const double* __restrict__ fx, double2* __restrict__ Hx,
-    double2* __restrict__ wrows) {
+    double2* __restrict__ wrows, const double* __restrict__ cp, int ncp,
+    double* __restrict__ csout) {
   using P = Plan<L>;
   constexpr int THREADS = XR * P::T, PAIRS = (L / 2) * XR / THREADS;
   __shared__ double lds[XR * P::PAD];
@@ -779,7 +813,25 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
   const TwGlobal<2 * L> twN{twN_};
   const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
   double* buf = lds + q * P::PAD;
-  int y0 = xcd_remap(blockIdx.x, gridDim.x) * XR;
+  int bid = blockIdx.x, nbl = gridDim.x;
+  if constexpr (COL0 && THREADS == 256) {
+    if (cp != nullptr) {
+      // the first 2L/64 workgroups (dispatched first: their chain of load round trips runs
+      // beside the row items instead of after them): 64 columns each of the field's
+      // column-sum partial rows added up -- no transform, the sums travel with the
+      // all-gather; as a launch of its own this costs 5 us on the step
+      constexpr int NCS = (2 * L + 63) / 64;
+      if (bid < NCS) {
+        const int x0 = bid * 64;
+        const double t = colsum_block(cp, ncp, 2 * L, x0, reinterpret_cast<double(*)[64]>(lds));
+        if (threadIdx.x < 64 && x0 + (int)threadIdx.x < 2 * L) csout[x0 + threadIdx.x] = t;
+        return;
+      }
+      bid -= NCS;
+      nbl -= NCS;
+    }
+  }
+  int y0 = xcd_remap(bid, nbl) * XR;
   bool extra = false;
   if constexpr (COL0) {
     if (y0 >= M) {  // the one block whose index the (bijective) remap puts beyond the rows
@@ -1062,10 +1114,13 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
         if (pass == 0) {
           if ((a.fx && !(a.col0 && a.Hx)) || (a.wrows && !a.col0))
             throw Error{CFDJ_ERR_ARG, "fused Poisson: extra row without dense column 0"};
-          const dim3 gridx(a.rows / XR + (a.fx ? 1 : 0));
+          if (a.cp && (a.fx || !a.col0 || !a.csout || a.ncp < 1 || XR * Plan<L>::T != 256))
+            throw Error{CFDJ_ERR_ARG, "fused Poisson: column sums unsupported here"};
+          const dim3 gridx(a.rows / XR + (a.fx ? 1 : 0) + (a.cp ? (2 * L + 63) / 64 : 0));
           auto fwd = [&](auto nt, auto c0) {
             hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, true, nt.value, c0.value>), gridx, block,
-                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0, a.fx, a.Hx, a.wrows);
+                               0, st, a.f, a.H, a.rows, a.twL, a.twN, a.col0, a.fx, a.Hx, a.wrows,
+                               a.cp, a.ncp, a.csout);
           };
           using T = std::true_type;
           using F = std::false_type;
@@ -1098,10 +1153,12 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
           const dim3 grid(a.rows / XR), block(XR * Plan<L>::T);
           if (a.stream)
             hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, false, true>), grid, block, 0, st, a.f,
-                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr, nullptr);
+                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                               nullptr);
           else
             hipLaunchKernelGGL((rows_fwd_np_kernel<L, XR, false, false>), grid, block, 0, st, a.f,
-                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr, nullptr);
+                               a.H, a.rows, a.twL, a.twN, nullptr, nullptr, nullptr, nullptr, nullptr, 0,
+                               nullptr);
         } else {
           throw Error{CFDJ_ERR_ARG, "CFDJ_FWD_NP: workgroup too large for this row length"};
         }
@@ -1200,24 +1257,47 @@ bool fused_poisson_supported(int nx, int ny, int rows) {
 
 bool col0_solve_supported(int ny) { return pow2(ny) && ny >= 1024 && ny <= 8192; }
 
-void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg_stride,
-                       int rows, double2* dst, hipStream_t st) {
-  if (!col0_solve_supported(a.ny) || rows < 1 || !pow2(rows) || a.ny % rows != 0 ||
-      a.cy_mirror != nullptr)
-    throw Error{CFDJ_ERR_ARG, "packed column solve: unsupported size"};
-  const DivArgs da{a.cx,  a.cy,  nullptr,           a.aa, a.bb, a.cc,       a.scale,
-                   a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, 0, ilog2(rows), 0u};
-  const int rl_log2 = ilog2(rows);
+static bool col0_split_on() {
   static const bool split = [] {
     const char* e = std::getenv("CFDJ_COL0_SPLIT");
     return e ? e[0] != '0' : CFDJ_COL0_SPLIT != 0;
   }();
-  if (split && rows >= 2) {
+  return split;
+}
+
+bool col0_solve_takes_colsum(int nx, int ny, int rows) {
+  return nx == ny && col0_solve_supported(ny) && col0_split_on() && rows >= 2;
+}
+
+bool fused_rows_take_colsum(int nx, int rows) {
+  if (!fused_rows_take_col0(nx, rows)) return false;
+  switch (nx / 2) {  // the row pass's workgroup: 256 threads
+    case 512: return rows_np_xr<512, true>() * Plan<512>::T == 256;
+    case 1024: return rows_np_xr<1024, true>() * Plan<1024>::T == 256;
+    case 2048: return rows_np_xr<2048, true>() * Plan<2048>::T == 256;
+    case 4096: return rows_np_xr<4096, true>() * Plan<4096>::T == 256;
+    default: return false;
+  }
+}
+
+void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg_stride,
+                       int rows, double2* dst, hipStream_t st, const double2* cs_src,
+                       int nranks, double2* csT) {
+  if (!col0_solve_supported(a.ny) || rows < 1 || !pow2(rows) || a.ny % rows != 0 ||
+      a.cy_mirror != nullptr)
+    throw Error{CFDJ_ERR_ARG, "packed column solve: unsupported size"};
+  if (cs_src && (!col0_solve_takes_colsum(a.nx, a.ny, rows) || nranks < 1 || !csT))
+    throw Error{CFDJ_ERR_ARG, "packed column solve: column sums unsupported here"};
+  const DivArgs da{a.cx,  a.cy,  nullptr,           a.aa, a.bb, a.cc,       a.scale,
+                   a.nx / 2, a.neg ? 1 : 0, a.recip ? 1 : 0, 0, ilog2(rows), 0u};
+  const int rl_log2 = ilog2(rows);
+  if (col0_split_on() && rows >= 2) {
+    const dim3 g(cs_src ? 3 : 2);
     switch (a.ny) {
-      case 1024: hipLaunchKernelGGL((col0_split_kernel<1024>), dim3(2), dim3(Plan<512>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
-      case 2048: hipLaunchKernelGGL((col0_split_kernel<2048>), dim3(2), dim3(Plan<1024>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
-      case 4096: hipLaunchKernelGGL((col0_split_kernel<4096>), dim3(2), dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
-      default: hipLaunchKernelGGL((col0_split_kernel<8192>), dim3(2), dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da); break;
+      case 1024: hipLaunchKernelGGL((col0_split_kernel<1024>), g, dim3(Plan<512>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
+      case 2048: hipLaunchKernelGGL((col0_split_kernel<2048>), g, dim3(Plan<1024>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
+      case 4096: hipLaunchKernelGGL((col0_split_kernel<4096>), g, dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
+      default: hipLaunchKernelGGL((col0_split_kernel<8192>), g, dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
     }
     CFDJ_HIP(hipGetLastError());
     return;

@@ -114,13 +114,14 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
     }
     const double2 fsep = tile[mi];
     const double mdy2 = -1.0 / a.inv_dy2;
-    double2* out = a.T + (size_t)a.rank * a.tstride + (size_t)m * 4;
+    double2* out = a.T + (size_t)a.rank * a.tstride + (size_t)m * a.tnum;
     out[0] = fsep;
     out[1] = cscale(t1, mdy2);
     out[2] = cscale(tn, mdy2);
     // column sum over all rows of the slab, separator included: the row r2c of the
-    // slab's column-sum row (element (m, 0) of the 8-row tile spectrum a.cs)
-    out[3] = a.cs[((size_t)(m >> 3) << 6) + (m & 7)];
+    // slab's column-sum row (element (m, 0) of the 8-row tile spectrum a.cs) -- unless the
+    // sums travel untransformed and the solve gets the total's spectrum (tnum == 3)
+    if (a.tnum == 4) out[3] = a.cs[((size_t)(m >> 3) << 6) + (m & 7)];
   }
 }
 
@@ -173,13 +174,14 @@ __global__ __launch_bounds__(MW * K) void schur_solve_kernel(const SchurArgs a) 
   double2 sp = make_double2(0.0, 0.0), sq = sp, fb = sp;
   const double* ci = a.cinv + (size_t)mm * a.P;
   for (int qq = 0; qq < a.P; ++qq) {
-    const double2* Tq = a.T + (size_t)qq * a.tstride + (size_t)mm * 4;
-    const double2* Tm = a.T + (size_t)((qq + a.P - 1) % a.P) * a.tstride + (size_t)mm * 4;
+    const double2* Tq = a.T + (size_t)qq * a.tstride + (size_t)mm * a.tnum;
+    const double2* Tm = a.T + (size_t)((qq + a.P - 1) % a.P) * a.tstride + (size_t)mm * a.tnum;
     const double2 rhs = csub(Tq[0], cscale(cadd(Tm[2], Tq[1]), a.inv_dy2));
     sp = cadd(sp, cscale(rhs, ci[(qq - a.rank + a.P) % a.P]));
     sq = cadd(sq, cscale(rhs, ci[(qq - a.rank - 1 + 2 * a.P) % a.P]));
-    fb = cadd(fb, Tq[3]);
+    if (a.csT == nullptr) fb = cadd(fb, Tq[3]);
   }
+  if (a.csT != nullptr) fb = a.csT[mm];
   const double2 cst = cscale(fb, a.corr[mm] * a.inv_ny);
 
   // chunk rows, scaled by dy^2

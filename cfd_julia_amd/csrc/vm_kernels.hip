@@ -11,6 +11,7 @@
 // bit-identical to the CPU oracle (oracle/vm_oracle.py: arakawa_rhs, rk3_step).
 #include <cstdlib>
 
+#include "colsum.hpp"
 #include "stencil.hpp"
 
 namespace cfdj {
@@ -413,23 +414,9 @@ __global__ __launch_bounds__(256) void colsum_row_kernel(const double* __restric
   __shared__ double part[4][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int x = blockIdx.x * 64 + lane;
-  double s = 0.0;
-  if (x < nx) {
-    // eight loads in flight per lane, added in the order of the plain loop
-    int b = w;
-    for (; b + 28 < nb; b += 32) {
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = colpart[(size_t)(b + 4 * u) * nx + x];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; b < nb; b += 4) s += colpart[(size_t)b * nx + x];
-  }
-  part[w][lane] = s;
-  __syncthreads();
+  const double t = colsum_block(colpart, nb, nx, blockIdx.x * 64, part);
   if (x >= nx) return;
-  if (w == 0) out8[x] = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+  if (w == 0) out8[x] = t;
   else out8[(size_t)w * nx + x] = 0.0;
   out8[(size_t)(w + 4) * nx + x] = 0.0;
 }

@@ -208,3 +208,30 @@ def test_gpu_virtual_slabs_tall_tile_stage_kernel_matches_marching(cfdj, monkeyp
     if n <= 2048:
         ref = vo.numerical(w0, 3, dt, dx, dy, 1000.0)
         assert np.abs(out["tall"] - ref).max() < 1e-10
+
+
+@pytest.mark.parametrize("n,P", [(1024, 2), (2048, 4), (4096, 8), (4096, 1)])
+def test_gpu_schur_column_sums_transformed_after_the_gather(cfdj, monkeypatch, n, P):
+    """The constant-mode correction needs the spectrum of the field's column sum over ALL rows.
+    Default: every slab's untransformed sums ride in the all-gather (added up from the stage
+    kernel's partial rows by extra workgroups of the forward row pass) and one more workgroup
+    of the packed column's solve adds the ranks' rows and transforms the total.
+    CFDJ_SLAB_LATE_CS=0: a summing launch and a transform per slab before the gather, the
+    solve adding the spectra.  The correction is ~1e-8 of psi, so psi must agree far below the
+    oracle tolerance (1e-14 of max|psi|), and both routes stay within it."""
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w = vo.vm_ic(n, n, x, y) + 0.01 * np.random.default_rng(7 * n + P).standard_normal((n, n))
+    ref = vo.fps(-w, dx, dy)
+    out = {}
+    for late in ("1", "0"):
+        monkeypatch.setenv("CFDJ_SLAB_LATE_CS", late)
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+            assert h.poisson() == "schur"
+            _, s = h.rhs(vo.to_ghosted(w))
+        out[late] = vo.from_ghosted(s)
+    scale = np.abs(ref).max()
+    assert np.abs(out["1"] - out["0"]).max() <= 1e-14 * scale
+    tol = 4e-12 * (n / 1024) ** 2 * scale
+    assert np.abs(out["1"] - ref).max() <= tol
+    # a correction left out would be visible: the y-constant part of psi differs from the
+    # circulant's by ~1e-8 relative
