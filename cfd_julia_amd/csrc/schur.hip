@@ -45,9 +45,18 @@ __device__ __forceinline__ double2 cscale(double2 a, double s) { return make_dou
 #define CFDJ_TRACE_THREADS 256
 #endif
 constexpr int kTraceThreads = CFDJ_TRACE_THREADS;
+#ifndef CFDJ_TRACE_MODES
+#define CFDJ_TRACE_MODES 8
+#endif
+// Modes per workgroup (8 = a whole tile, 128-B row pieces; fewer = more row lanes per mode).
+// The kernel's duration is its slowest workgroup's: the lowest modes' tiles read their whole
+// column, rl / (threads / modes) rows per lane in batches of U with a load round trip each.
+constexpr int kTraceModes = CFDJ_TRACE_MODES;
 __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurArgs a) {
-  const int tb = xcd_remap(blockIdx.x, gridDim.x);  // tile: modes 8 tb .. 8 tb + 7
-  const int mi = threadIdx.x & 7, r0 = threadIdx.x >> 3;
+  constexpr int MPW = kTraceModes, PER = 8 / MPW;
+  const int lb = xcd_remap(blockIdx.x, gridDim.x);
+  const int tb = lb / PER;  // tile: modes 8 tb .. 8 tb + 7
+  const int mi = (lb % PER) * MPW + threadIdx.x % MPW, r0 = threadIdx.x / MPW;
   const int m = 8 * tb + mi;
   const int rl = a.rl;
   const double2* tile = a.H + (((size_t)tb * rl) << 3);
@@ -57,11 +66,14 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
   // column sum comes from the stage kernel's column partials (a.cs), not from this pass
   double2 t1 = make_double2(0.0, 0.0), tn = t1;
   const int J = a.jt[tb];
-  constexpr int RS = kTraceThreads / 8;
+  constexpr int RS = kTraceThreads / MPW;
   // loads in batches of U rows per lane (the lane's rows still summed in increasing j, so
   // the result does not depend on U): the slowest tiles' full-column loop is load-latency
   // bound, one batch in flight per iteration
-  constexpr int U = 8;
+#ifndef CFDJ_TRACE_U
+#define CFDJ_TRACE_U 8
+#endif
+  constexpr int U = CFDJ_TRACE_U;
   auto sweep = [&](int jb, int je, bool first, bool last) {
     for (int j0 = jb + r0; j0 < je; j0 += U * RS) {
       double2 f[U];
@@ -90,27 +102,27 @@ __global__ __launch_bounds__(kTraceThreads) void schur_trace_kernel(const SchurA
     sweep(1, J + 1, true, false);
     sweep(rl - J, rl, false, true);
   }
-  // sum over the 8 row lanes of a wavefront with the same mode, then over the 4 waves
+  // sum over the row lanes of a wavefront with the same mode, then over the waves
 #pragma unroll
-  for (int o = 8; o < 64; o <<= 1) {
+  for (int o = MPW; o < 64; o <<= 1) {
     t1.x += __shfl_xor(t1.x, o);
     t1.y += __shfl_xor(t1.y, o);
     tn.x += __shfl_xor(tn.x, o);
     tn.y += __shfl_xor(tn.y, o);
   }
   constexpr int W = kTraceThreads / 64;
-  __shared__ double2 red[2][W][8];
+  __shared__ double2 red[2][W][MPW];
   const int wv = threadIdx.x / 64, ln = threadIdx.x % 64;
-  if (ln < 8) {
+  if (ln < MPW) {
     red[0][wv][ln] = t1;
     red[1][wv][ln] = tn;
   }
   __syncthreads();
-  if (threadIdx.x < 8 && m >= 1) {
+  if (threadIdx.x < MPW && m >= 1) {
     t1 = tn = make_double2(0.0, 0.0);
     for (int w = 0; w < W; ++w) {
-      t1 = cadd(t1, red[0][w][mi]);
-      tn = cadd(tn, red[1][w][mi]);
+      t1 = cadd(t1, red[0][w][threadIdx.x]);
+      tn = cadd(tn, red[1][w][threadIdx.x]);
     }
     const double2 fsep = tile[mi];
     const double mdy2 = -1.0 / a.inv_dy2;
@@ -310,7 +322,7 @@ __global__ __launch_bounds__(256) void packed_divide_kernel(const PackedDivParam
 template <int K>
 void launch_schur_n(int pass, const SchurArgs& a, hipStream_t st) {
   if (pass == 0)
-    hipLaunchKernelGGL(schur_trace_kernel, dim3(a.L / 8), dim3(kTraceThreads), 0, st, a);
+    hipLaunchKernelGGL(schur_trace_kernel, dim3(a.L / kTraceModes), dim3(kTraceThreads), 0, st, a);
   else
   {
 #ifndef CFDJ_SCHUR_MW64
