@@ -434,12 +434,14 @@ struct cfdj_vm {
   }
 
   // y-slabs without a transpose (schur.hip): row r2c -> interior traces -> ONE all-gather of
-  // every rank's traces (4 numbers per x-mode) and its piece of the packed DC / Nyquist column
-  // -> that column's solve (one workgroup) -> separator + interior solve -> row c2r.
-  // The gather buffer TG holds one block per rank, [4 L trace numbers][rows column elements];
-  // a rank's own block is where its kernels write (in-place all-gather).  The packed column
-  // is solved with the reference symbol: columns of up to 8192 by col0_solve_kernel straight
-  // from the blocks, longer ones by library transforms on the dense copy G.
+  // every rank's traces, its piece of the packed DC / Nyquist column and (where the row pass
+  // supplies them) its column sums and its first and last input rows -> that column's solve
+  // -> separator + interior solve -> row c2r.  The gather buffer TG holds one block per rank,
+  // [4 L: 4 trace numbers per x-mode, or 3 and then the L column sums][rows column elements]
+  // [L first row][L last row]; a rank's own block is where its kernels write (in-place
+  // all-gather).  The packed column is solved with the reference symbol: columns of up to
+  // 8192 by launch_col0_solve straight from the blocks, longer ones by library transforms on
+  // the dense copy G.
   void poisson_schur(const std::vector<const double*>& src, bool neg) {
     const int L = nx / 2;
     const double out_scale = (neg ? -1.0 : 1.0) / (double)nx;
