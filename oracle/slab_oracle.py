@@ -21,18 +21,22 @@ from . import vm_oracle as vo
 
 
 class LocalComm:
-    """P virtual ranks in one process (lists of per-rank arrays)."""
+    """P virtual ranks in one process (lists of per-rank arrays).  `calls` counts the
+    collectives by kind."""
 
     def __init__(self, P):
         self.P = P
+        self.calls = {"alltoall": 0, "allgather": 0}
 
     def alltoall(self, chunks):
         # chunks[p][q] (rank p's chunk for rank q) -> out[q][p]
         P = self.P
+        self.calls["alltoall"] += 1
         return {q: [chunks[p][q] for p in range(P)] for q in range(P)}
 
     def allgather(self, parts):
         # parts[p] (rank p's array) -> [parts[0], ..., parts[P-1]]
+        self.calls["allgather"] += 1
         return [parts[p] for p in range(self.P)]
 
 
@@ -45,9 +49,11 @@ class DistComm:
         self.P = dist.get_world_size()
         self.rank = dist.get_rank()
         self.local_ranks = [self.rank]
+        self.calls = {"alltoall": 0, "allgather": 0, "halo": 0}
 
     def alltoall(self, chunks):
         import torch
+        self.calls["alltoall"] += 1
         mine = chunks[self.rank]
         shape = mine[0].shape
         send = torch.from_numpy(np.ascontiguousarray(np.stack(mine)).view(np.float64).copy())
@@ -58,6 +64,7 @@ class DistComm:
 
     def allgather(self, parts):
         import torch
+        self.calls["allgather"] += 1
         mine = np.ascontiguousarray(parts[self.rank])
         t = torch.from_numpy(mine.view(np.float64).copy())
         out = [torch.empty_like(t) for _ in range(self.P)]
@@ -66,6 +73,7 @@ class DistComm:
 
     def halo(self, slabs):
         import torch
+        self.calls["halo"] += 1
         (w,) = slabs
         P, r = self.P, self.rank
         prev, nxt = (r - 1) % P, (r + 1) % P
@@ -180,6 +188,93 @@ def slab_poisson_schur(w_slabs, nx, ny, dx, dy, eps, comm, neg=True, workers=1):
         X[ms] = so.slab_solve(F[p][ms], lam, T, p, c, ms, dy, ny)
         out.append(sfft.irfft(X, n=nx, axis=0, workers=workers))
     return out
+
+
+def slab_poisson_schur_one_gather(w_slabs, nx, ny, dx, dy, eps, comm, neg=True, workers=1):
+    """The substructured solve as cfdj_vm::poisson_schur runs it by default: ONE all-gather per
+    solve whose block per rank is [3 trace numbers per x-mode 1..L-1][the slab's column sums,
+    nx reals, untransformed][its piece of the x-mode 0 and nx/2 columns][its first and last
+    input rows]; no other communication.  Returns, per local rank, (psi, psi_lo, psi_hi, w_lo,
+    w_hi): the slab and the four halo rows the stencil needs --
+      w_lo / w_hi   the neighbours' last / first rows, taken out of the gathered blocks;
+      psi_hi        the row after the slab = the next slab's separator row, whose value s_q
+                    every rank has from the separator system;
+      psi_lo        the row before the slab, from the operator's equation at the slab's own
+                    separator row: (psi[-1] + psi[1]) / dy^2 + d_m psi[0] = f[0] per x-mode;
+    the x-modes 0 and nx/2 of both rows come from the solved gathered column; the constant-mode
+    correction from the transform of the ranks' column sums added up AFTER the gather."""
+    from . import schur_oracle as so
+
+    P = comm.P
+    rows = ny // P
+    L = nx // 2
+    ranks = getattr(comm, "local_ranks", list(range(P)))
+    c = so.mode_constants(nx, ny, dx, dy, P, eps)
+    ms, lam = so.interior_lambda(c)
+    sgn = -1.0 if neg else 1.0
+    F = {p: sfft.rfft(sgn * w_slabs[i], axis=0, workers=workers) for i, p in enumerate(ranks)}
+
+    def block(i, p):
+        tr = so.slab_traces(F[p][ms], lam)[:3]  # separator row, the two interior traces
+        cs = (sgn * w_slabs[i]).sum(axis=1)      # column sums of the slab, physical space
+        return np.concatenate([tr.ravel(), cs.astype(np.complex128), F[p][0], F[p][L],
+                               w_slabs[i][:, 0].astype(np.complex128),
+                               w_slabs[i][:, -1].astype(np.complex128)])
+
+    blocks = comm.allgather({p: block(i, p) for i, p in enumerate(ranks)})
+    nm = len(ms)
+    o_cs, o_c0, o_cL, o_w0, o_w1 = 3 * nm, 3 * nm + nx, 3 * nm + nx + rows, \
+        3 * nm + nx + 2 * rows, 3 * nm + 2 * nx + 2 * rows
+    T = [b[:o_cs].reshape(3, nm) for b in blocks]
+    cs_hat = sfft.rfft(sum(b[o_cs:o_c0].real for b in blocks))[ms]  # rank 0 first
+    g0 = so.column_solve(np.concatenate([b[o_c0:o_cL] for b in blocks]), c, 0, eps)
+    gL = so.column_solve(np.concatenate([b[o_cL:o_w0] for b in blocks]), c, L, eps)
+    dy2 = dy * dy
+    out = []
+    for i, p in enumerate(ranks):
+        # slab_solve wants the column sums per rank in T[q][3]: hand it the total once
+        T4 = [np.vstack([T[q], cs_hat if q == 0 else np.zeros(nm)]) for q in range(P)]
+        core = so.slab_solve(F[p][ms], lam, T4, p, c, ms, dy, ny)
+        cst = (cs_hat / ny) * c["corr"][ms]
+        X = np.empty_like(F[p])
+        X[0] = g0[p * rows:(p + 1) * rows]
+        X[L] = gL[p * rows:(p + 1) * rows]
+        X[ms] = core
+        psi = sfft.irfft(X, n=nx, axis=0, workers=workers)
+        # the two rows just outside the slab
+        rhs = np.stack([T[q][0] - (T[(q - 1) % P][2] + T[q][1]) / dy2 for q in range(P)])
+        sq = np.einsum("mq,qm->m", c["minv"][ms][:, (p + 1) % P, :], rhs)
+        u0, u1 = core[:, 0] - cst, core[:, 1] - cst  # T^{-1} f at rows 0 and 1
+        lo = dy2 * (F[p][ms, 0] - c["d"][ms] * u0) - u1
+        Xlo, Xhi = np.zeros(L + 1, dtype=np.complex128), np.zeros(L + 1, dtype=np.complex128)
+        Xlo[ms], Xhi[ms] = lo + cst, sq + cst
+        jlo, jhi = (p * rows - 1) % ny, ((p + 1) * rows) % ny
+        Xlo[0], Xlo[L], Xhi[0], Xhi[L] = g0[jlo], gL[jlo], g0[jhi], gL[jhi]
+        w_lo = blocks[(p - 1) % P][o_w1:].real
+        w_hi = blocks[(p + 1) % P][o_w0:o_w1].real
+        out.append((psi, sfft.irfft(Xlo, n=nx), sfft.irfft(Xhi, n=nx), w_lo, w_hi))
+    return out
+
+
+def slab_rk3_step_one_gather(wn, dt, nx, ny, dx, dy, re, eps, comm):
+    """One RK3 step whose only communication is the solve's all-gather, three per step
+    (slab_poisson_schur_one_gather): the stencil's halo rows come with the solve."""
+
+    def rhs(w):
+        out = []
+        for wi, (s, sl, sh, wl, wh) in zip(w, slab_poisson_schur_one_gather(
+                w, nx, ny, dx, dy, eps, comm)):
+            we = np.concatenate([wl[:, None], wi, wh[:, None]], axis=1)
+            se = np.concatenate([sl[:, None], s, sh[:, None]], axis=1)
+            out.append(vo.arakawa_rhs(we, se, dx, dy, re)[:, 1:-1])
+        return out
+
+    r = rhs(wn)
+    wt = [a + dt * b for a, b in zip(wn, r)]
+    r = rhs(wt)
+    wt = [(0.75 * a + 0.25 * b) + (0.25 * dt) * c for a, b, c in zip(wn, wt, r)]
+    r = rhs(wt)
+    return [(a / 3.0 + (2.0 / 3.0) * b) + ((2.0 / 3.0) * dt) * c for a, b, c in zip(wn, wt, r)]
 
 
 def halo_rows(slabs, comm):

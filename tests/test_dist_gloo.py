@@ -34,8 +34,13 @@ def _worker(rank, ws, port, nx, nsteps, q, poisson="transpose"):
         comm = so.DistComm()
         mine = [so.split(w, ws)[rank]]
         for _ in range(nsteps):
-            mine = so.slab_rk3_step(mine, 0.01, nx, ny, dx, dy, 1000.0, 1e-6, comm,
-                                    poisson=poisson)
+            if poisson == "one-gather":
+                mine = so.slab_rk3_step_one_gather(mine, 0.01, nx, ny, dx, dy, 1000.0, 1e-6, comm)
+            else:
+                mine = so.slab_rk3_step(mine, 0.01, nx, ny, dx, dy, 1000.0, 1e-6, comm,
+                                        poisson=poisson)
+        if poisson == "one-gather":  # three solves per step, nothing else on the wire
+            assert comm.calls == {"alltoall": 0, "allgather": 3 * nsteps, "halo": 0}, comm.calls
         # gather the slabs on rank 0 and compare with the single-domain oracle
         import torch
 
@@ -71,6 +76,46 @@ def test_schur_slab_decomposition_matches_single_domain(ws, nx):
                        start_method="spawn", join=True)
     err = q.get(timeout=5)
     assert err < 1e-13, err
+
+
+@pytest.mark.parametrize("ws,nx", [(2, 64), (4, 64)])
+def test_one_gather_stage_matches_single_domain(ws, nx):
+    """The y-slab step as libcfdj.so runs it on the substructured path: one all-gather per
+    solve carries the traces, the untransformed column sums, the packed-column pieces and the
+    first / last vorticity rows; psi's halo rows come out of the slab's own solve.  Over real
+    process groups: the single-domain oracle to round-off, and exactly three collectives per
+    step (asserted in the worker)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    mp.start_processes(_worker, args=(ws, port, nx, 3, q, "one-gather"), nprocs=ws,
+                       start_method="spawn", join=True)
+    err = q.get(timeout=5)
+    assert err < 1e-13, err
+
+
+def test_one_gather_halo_rows_are_the_neighbours_rows():
+    """The halo rows the one-gather solve returns, against the neighbouring slabs' own rows
+    (what the exchanging schedule would have sent), P = 1, 2, 4, 8."""
+    from oracle import slab_oracle as so
+    from oracle import vm_oracle as vo
+
+    n = 128
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w = vo.vm_ic(n, n, x, y) + 0.05 * np.random.default_rng(3).standard_normal((n, n))
+    for P in (1, 2, 4, 8):
+        comm = so.LocalComm(P)
+        ws = so.split(w, P)
+        res = so.slab_poisson_schur_one_gather(ws, n, n, dx, dy, 1e-6, comm)
+        assert comm.calls == {"alltoall": 0, "allgather": 1}
+        ref = so.slab_poisson_schur(ws, n, n, dx, dy, 1e-6, so.LocalComm(P))
+        scale = np.abs(np.concatenate(ref, axis=1)).max()
+        for p, (psi, slo, shi, wlo, whi) in enumerate(res):
+            assert np.abs(psi - ref[p]).max() < 1e-13 * scale
+            assert np.abs(slo - ref[(p - 1) % P][:, -1]).max() < 1e-12 * scale
+            assert np.abs(shi - ref[(p + 1) % P][:, 0]).max() < 1e-12 * scale
+            assert np.array_equal(wlo, ws[(p - 1) % P][:, -1])
+            assert np.array_equal(whi, ws[(p + 1) % P][:, 0])
 
 
 def test_schur_oracle_matches_fps():
