@@ -548,8 +548,12 @@ def main(argv=None):
     value = cells * args.steps / elapsed / 1e6
     ms_step = elapsed * 1e3 / args.steps
     local_cells = cells / n_gpus
+    # cells one stage-kernel launch covers: a slab (virtual slabs: one launch per slab)
+    launch_cells = local_cells / max(args.virtual, 1)
     kname = "vm_stage"
-    stage_kernel = "vm_stage_tile_kernel<1..3>" if stage_tile else "vm_stage_kernel<1..3>"
+    stage_kernel = ("vm_stage_tile_kernel<1..3>" if stage_tile else
+                    "vm_stage_tall_kernel / vm_stage_kernel<1..3>" if kind != "single" else
+                    "vm_stage_kernel<1..3>")
     # Roofline of the stage kernels from their IN-STEP launch times: HIP events around every
     # stage-kernel launch of the instrumented timed region (the kernels run in the step's
     # own sequence, between the Poisson passes), algorithmic bytes 24 / 32 / 32 per cell
@@ -559,14 +563,14 @@ def main(argv=None):
     for i, (ms_i, n_i) in enumerate(kern_stage):
         if n_i:
             us_i = ms_i * 1e3 / n_i
-            gbs_i = alg_cell[i] * local_cells / (us_i * 1e-6) / 1e9
+            gbs_i = alg_cell[i] * launch_cells / (us_i * 1e-6) / 1e9
             per_stage.append({"stage": i + 1, "avg_launch_us": round(us_i, 2),
-                              "alg_bytes": int(alg_cell[i] * local_cells),
+                              "alg_bytes": int(alg_cell[i] * launch_cells),
                               "achieved": round(gbs_i, 1),
                               "frac": round(gbs_i / HBM_PEAK_GBS, 4), "launches": n_i})
     stage_ms, stage_n = kern["stage"]
     stage_us = stage_ms * 1e3 / max(stage_n, 1)
-    stage_alg = sum(alg_cell) / 3.0 * local_cells
+    stage_alg = sum(alg_cell) / 3.0 * launch_cells
     source = ("HIP events around every stage-kernel launch on the handle stream, in the "
               "step's own kernel sequence, over one more timed region of the same K steps "
               "(eager launches); mean over the three RK3 stages")
@@ -642,8 +646,12 @@ def main(argv=None):
         if not args.no_ladders:
             sx, sy, _, _ = grid_for(n_gpus, strong=4096)
             wx, wy, _, _ = grid_for(n_gpus, "weak")
-            for key, (gx, gy) in (("c5_8192", (8192, 8192)), ("strong_4096", (sx, sy)),
-                                  ("weak", (wx, wy))):
+            rungs = [("c5_8192", (8192, 8192)), ("strong_4096", (sx, sy)), ("weak", (wx, wy))]
+            if n_gpus in (4, 8):
+                # aggregate-throughput rung: the largest square grid of the substructured path
+                # (67 / 33.5 M cells per GPU at N = 4 / 8 -- more work per GPU than n1's)
+                rungs.append(("square_16384", (16384, 16384)))
+            for key, (gx, gy) in rungs:
                 if (gx, gy) == (nx, ny) and args.poisson == "auto" and not args.rows_per_wave:
                     entry = dict(head)
                 else:
@@ -654,7 +662,7 @@ def main(argv=None):
                 ladders[key] = entry
             ladders["efficiency_rule"] = ("mlups / (n_gpus x n1_reference.mlups): strong "
                                           "ladders at fixed total work, weak at fixed work "
-                                          "per GPU")
+                                          "per GPU, square_16384 at 2-4x n1's work per GPU")
         line["ladders"] = ladders
         line["multi_rank_parity"] = parity
         if parity and not parity["linf_rel"] < parity["tolerance"]:

@@ -814,7 +814,7 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
   const int q = threadIdx.x / P::T, tid = threadIdx.x % P::T;
   double* buf = lds + q * P::PAD;
   int bid = blockIdx.x, nbl = gridDim.x;
-  if constexpr (COL0 && THREADS == 256) {
+  if constexpr (COL0 && THREADS >= 256) {
     if (cp != nullptr) {
       // the first 2L/64 workgroups (dispatched first: their chain of load round trips runs
       // beside the row items instead of after them): 64 columns each of the field's
@@ -1106,7 +1106,7 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
 #if CFDJ_ROWS_INV_NP > 0
   // the small-item kernels: the inverse pass in both layouts, the forward pass in the
   // 8-mode-tile layout; rows of up to 4096 (column-major) / 8192 (tiles) reals
-  if constexpr (L <= 4096) {
+  if constexpr (L <= 8192) {
     if (a.tile8) {
       constexpr int XR = rows_np_xr<L, true>();
       if (a.rows % XR == 0) {
@@ -1114,7 +1114,7 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
         if (pass == 0) {
           if ((a.fx && !(a.col0 && a.Hx)) || (a.wrows && !a.col0))
             throw Error{CFDJ_ERR_ARG, "fused Poisson: extra row without dense column 0"};
-          if (a.cp && (a.fx || !a.col0 || !a.csout || a.ncp < 1 || XR * Plan<L>::T != 256))
+          if (a.cp && (a.fx || !a.col0 || !a.csout || a.ncp < 1 || XR * Plan<L>::T < 256))
             throw Error{CFDJ_ERR_ARG, "fused Poisson: column sums unsupported here"};
           const dim3 gridx(a.rows / XR + (a.fx ? 1 : 0) + (a.cp ? (2 * L + 63) / 64 : 0));
           auto fwd = [&](auto nt, auto c0) {
@@ -1142,6 +1142,11 @@ void launch_rows(int pass, const FusedPoissonArgs& a, hipStream_t st) {
         }
         return;
       }
+    }
+  }
+  if constexpr (L <= 4096) {
+    if (a.tile8) {
+      // (taken above)
     } else if (pass == 0 && L <= 2048 && fwd_np_rows() > 0) {
       // A/B switch (CFDJ_FWD_NP=2|4|8): the forward pass in the small-item shape on the
       // column-major layout, XR rows per workgroup (column segments of 16 XR bytes)
@@ -1247,7 +1252,7 @@ bool fused_rows_supported(int nx, int rows) {
 
 // Whether the row passes of the 8-mode-tile layout take FusedPoissonArgs::col0.
 bool fused_rows_take_col0(int nx, int rows) {
-  return CFDJ_ROWS_INV_NP > 0 && fused_rows_supported(nx, rows) && nx <= 8192;
+  return CFDJ_ROWS_INV_NP > 0 && fused_rows_supported(nx, rows) && nx <= 16384;
 }
 
 bool fused_poisson_supported(int nx, int ny, int rows) {
@@ -1255,14 +1260,17 @@ bool fused_poisson_supported(int nx, int ny, int rows) {
          rows >= 8 && rows % 8 == 0 && ny % rows == 0;
 }
 
-bool col0_solve_supported(int ny) { return pow2(ny) && ny >= 1024 && ny <= 8192; }
-
 static bool col0_split_on() {
   static const bool split = [] {
     const char* e = std::getenv("CFDJ_COL0_SPLIT");
     return e ? e[0] != '0' : CFDJ_COL0_SPLIT != 0;
   }();
   return split;
+}
+
+// (16384: as two half-length real transforms only -- the whole column does not fit the LDS)
+bool col0_solve_supported(int ny) {
+  return pow2(ny) && ny >= 1024 && (ny <= 8192 || (ny == 16384 && col0_split_on()));
 }
 
 bool col0_solve_takes_colsum(int nx, int ny, int rows) {
@@ -1276,6 +1284,7 @@ bool fused_rows_take_colsum(int nx, int rows) {
     case 1024: return rows_np_xr<1024, true>() * Plan<1024>::T == 256;
     case 2048: return rows_np_xr<2048, true>() * Plan<2048>::T == 256;
     case 4096: return rows_np_xr<4096, true>() * Plan<4096>::T == 256;
+    case 8192: return rows_np_xr<8192, true>() * Plan<8192>::T == 512;
     default: return false;
   }
 }
@@ -1297,7 +1306,8 @@ void launch_col0_solve(const FusedPoissonArgs& a, const double2* src, size_t seg
       case 1024: hipLaunchKernelGGL((col0_split_kernel<1024>), g, dim3(Plan<512>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
       case 2048: hipLaunchKernelGGL((col0_split_kernel<2048>), g, dim3(Plan<1024>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
       case 4096: hipLaunchKernelGGL((col0_split_kernel<4096>), g, dim3(Plan<2048>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
-      default: hipLaunchKernelGGL((col0_split_kernel<8192>), g, dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
+      case 8192: hipLaunchKernelGGL((col0_split_kernel<8192>), g, dim3(Plan<4096>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
+      default: hipLaunchKernelGGL((col0_split_kernel<16384>), g, dim3(Plan<8192>::T), 0, st, src, seg_stride, rl_log2, dst, a.twM, da, cs_src, nranks, csT); break;
     }
     CFDJ_HIP(hipGetLastError());
     return;

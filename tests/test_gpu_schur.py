@@ -235,3 +235,33 @@ def test_gpu_schur_column_sums_transformed_after_the_gather(cfdj, monkeypatch, n
     assert np.abs(out["1"] - ref).max() <= tol
     # a correction left out would be visible: the y-constant part of psi differs from the
     # circulant's by ~1e-8 relative
+
+
+def test_gpu_schur_16384_steps_exchange_free_vs_exchanging_schedule(cfdj, monkeypatch):
+    """16384^2 on 8 slabs (rows and columns of 16384: the longest the small-item row kernels
+    and the split packed-column solve take): 2 steps of the default schedule -- one all-gather
+    per stage, psi's halo rows out of the solve, column sums transformed after the gather --
+    against the exchanging one with the per-slab column-sum transforms.  No oracle at this size;
+    the two schedules share the interior solve but not the halo rows' route, the packed
+    column's partner lookup or the correction's input, and must agree to round-off."""
+    n, P = 16384, 8
+    dx, dy, x, y = vo.vm_grid(n, n)
+    w0 = vo.vm_ic(n, n, x, y)
+    dt = 5e-4 * (4096 / n) ** 2
+    out = {}
+    for name, env in (("default", {}), ("exchange", {"CFDJ_SLAB_W_HALO": "exchange",
+                                                     "CFDJ_SLAB_PSI_HALO": "exchange",
+                                                     "CFDJ_SLAB_LATE_CS": "0"})):
+        for k in ("CFDJ_SLAB_W_HALO", "CFDJ_SLAB_PSI_HALO", "CFDJ_SLAB_LATE_CS"):
+            monkeypatch.delenv(k, raising=False)
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        with cfdj.VortexMerger(n, n, dx, dy, 1000.0, kind="virtual", nranks=P) as h:
+            assert h.poisson() == "schur"
+            h.upload_interior(w0)
+            h.step(dt, 2)
+            out[name] = h.download_interior()
+    scale = np.abs(out["exchange"]).max()
+    assert np.isfinite(out["default"]).all()
+    assert np.abs(out["default"] - out["exchange"]).max() <= 1e-12 * scale
+    assert np.abs(out["default"] - w0).max() > 1e-6 * scale  # (the field moved)

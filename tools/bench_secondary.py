@@ -178,7 +178,9 @@ def bench_rank_rehearsal(steps=20, single_ms=None):
                               ("strong 4096^2", 4096, 4096, 8),
                               ("config 5 8192^2", 8192, 8192, 2), ("config 5 8192^2", 8192, 8192, 4),
                               ("config 5 8192^2", 8192, 8192, 8),
-                              ("weak", 8192, 4096, 2), ("weak", 16384, 8192, 8)):
+                              ("weak", 8192, 4096, 2), ("weak", 16384, 8192, 8),
+                              ("square 16384^2", 16384, 16384, 8),
+                              ("square 16384^2", 16384, 16384, 4)):
         ms, path = run(nx, ny, P, True, True)
         cells = nx * ny // P
         out.append({"config": f"R {ladder}: rank 0 of {P}, {nx}x{ny} ({path})",
