@@ -682,6 +682,19 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 #ifndef CFDJ_ROWS_NP_XR_MIN
 #define CFDJ_ROWS_NP_XR_MIN 2
 #endif
+// Minimum wavefronts per SIMD the small-item row kernels are compiled for (1: no constraint).
+// Rows of 8192 complex points are 512-thread workgroups, two wavefronts per SIMD each, and
+// at their 142-154 registers only one fits a CU; the 128-register cap that admits a second
+// (CFDJ_ROWS_NP_WAVES_8192=4) spills 19-33 registers and measured 158-162 us per pass at
+// 16384 x 2048 against 147-148 without.
+#ifndef CFDJ_ROWS_NP_WAVES_8192
+#define CFDJ_ROWS_NP_WAVES_8192 1
+#endif
+template <int L>
+constexpr int rows_np_waves() {
+  return L >= 8192 ? CFDJ_ROWS_NP_WAVES_8192 : 1;
+}
+
 template <int L, bool TILE>
 constexpr int rows_np_xr() {
   constexpr int byT = 256 / Plan<L>::T;
@@ -707,7 +720,8 @@ struct HaloRows {
   const double2* c0hi;
 };
 template <int L, int XR, bool TILE, bool BAND = false, bool NTS = false, bool COL0 = false>
-__global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
+__global__ __launch_bounds__(XR* Plan<L>::T)
+    __attribute__((amdgpu_waves_per_eu(rows_np_waves<L>()))) void rows_inv_np_kernel(
     const double2* __restrict__ H, double* __restrict__ f, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_, int mmax,
     const double2* __restrict__ col0, const HaloRows hx) {
@@ -800,7 +814,8 @@ __global__ __launch_bounds__(XR* Plan<L>::T) void rows_inv_np_kernel(
 // the first XR rows of the 8-row array fx (the slab's column-sum row and zeros) into the
 // 8-row tiled spectrum Hx, which would otherwise be a launch of its own between two others.
 template <int L, int XR, bool TILE, bool NT, bool COL0 = false>
-__global__ __launch_bounds__(XR* Plan<L>::T) void rows_fwd_np_kernel(
+__global__ __launch_bounds__(XR* Plan<L>::T)
+    __attribute__((amdgpu_waves_per_eu(rows_np_waves<L>()))) void rows_fwd_np_kernel(
     const double* __restrict__ f, double2* __restrict__ H, int M,
     const double2* __restrict__ twL_, const double2* __restrict__ twN_,
     double2* __restrict__ col0, const double* __restrict__ fx, double2* __restrict__ Hx,
