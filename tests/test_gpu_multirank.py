@@ -2,8 +2,10 @@
 
 With one visible GPU only the one-rank form runs (the slab code over a one-rank
 communicator); the 2-, 4- and 8-rank forms need that many GPUs on the node and are skipped
-otherwise -- on such a node they are the parity test of the halo send/recv pairing and of
-the substructured solver's all-gathers against the oracle (tolerance 1e-10 of max|w|).
+otherwise -- on such a node they are the parity test against the oracle (tolerance 1e-10 of
+max|w|) of the substructured path's one all-gather per stage (traces, column sums, packed
+column, the neighbours' vorticity rows) and, in the "fused" case, of the transpose path's
+all-to-alls and its halo send/recv pairing.
 """
 import json
 import os
