@@ -359,7 +359,7 @@ class Job:
 
 
 FALLBACK_ENV = {"CFDJ_NO_OVERLAP": "1", "CFDJ_SLAB_W_HALO": "exchange",
-                "CFDJ_SLAB_PSI_HALO": "exchange"}
+                "CFDJ_SLAB_PSI_HALO": "exchange", "CFDJ_SLAB_LATE_CS": "0"}
 
 
 class Watchdog:

@@ -102,7 +102,7 @@ def test_parity_falls_back_to_the_single_stream_schedule():
     results = iter([{"linf_rel": 2e-3, "tolerance": 1e-10}, {"linf_rel": 4e-16, "tolerance": 1e-10}])
     got = bench.parity_with_fallback(lambda: next(results), env)
     assert env == {"CFDJ_NO_OVERLAP": "1", "CFDJ_SLAB_W_HALO": "exchange",
-                   "CFDJ_SLAB_PSI_HALO": "exchange"}
+                   "CFDJ_SLAB_PSI_HALO": "exchange", "CFDJ_SLAB_LATE_CS": "0"}
     assert got["schedule"].startswith("fallback: CFDJ_NO_OVERLAP=1") and got["linf_rel"] == 4e-16
     assert got["first_try"] == {"schedule": "default", "linf_rel": 2e-3}
     # not-a-number counts as a failure, and a second failure is reported as it is
