@@ -233,8 +233,20 @@ struct DstNpCfg {
   static constexpr int ENTRIES = (M2 / 4) * ROWS / THREADS;
 };
 
+// Minimum wavefronts per SIMD the inverse kernel is compiled for: at M2 = 4096 (256-thread
+// workgroups, 35 KB of LDS: four per CU) it wants 132 registers -- three workgroups per CU,
+// and the 1024 workgroups of a 2048^2 solve take one round and a third; 128 registers make it
+// one round.
+#ifndef CFDJ_DST_INV_NP_WAVES_4096
+#define CFDJ_DST_INV_NP_WAVES_4096 4
+#endif
 template <int M2>
-__global__ __launch_bounds__(DstNpCfg<M2>::THREADS) void dst_rows_inv_np_kernel(
+constexpr int dst_inv_np_waves() {
+  return M2 == 4096 ? CFDJ_DST_INV_NP_WAVES_4096 : 1;
+}
+template <int M2>
+__global__ __launch_bounds__(DstNpCfg<M2>::THREADS)
+    __attribute__((amdgpu_waves_per_eu(dst_inv_np_waves<M2>()))) void dst_rows_inv_np_kernel(
     const double2* __restrict__ T, int JT, double* __restrict__ s, int P, int ny,
     const double2* __restrict__ tw_, const double* __restrict__ sprev,
     double* __restrict__ part) {
