@@ -156,9 +156,18 @@ __device__ __forceinline__ void half_column(double* lds, const HalfSpecArgs& a,
 #ifndef CFDJ_HALF_COLS_WAVES
 #define CFDJ_HALF_COLS_WAVES 4
 #endif
+#ifndef CFDJ_HALF_COLS_WAVES_M3
+// mode 3 (four derivative spectra per column): 33 spilled registers at 4 waves per SIMD, none
+// at 3 -- and 139 us against 158 at 4096^2: occupancy wins
+#define CFDJ_HALF_COLS_WAVES_M3 4
+#endif
+template <int MODE>
+constexpr int half_cols_waves() {
+  return MODE == 3 ? CFDJ_HALF_COLS_WAVES_M3 : CFDJ_HALF_COLS_WAVES;
+}
 template <int M, int MODE, bool NT>
 __global__ __launch_bounds__(Plan<M>::T)
-    __attribute__((amdgpu_waves_per_eu(CFDJ_HALF_COLS_WAVES, CFDJ_HALF_COLS_WAVES))) void half_cols_kernel(const HalfSpecArgs a,
+    __attribute__((amdgpu_waves_per_eu(half_cols_waves<MODE>(), half_cols_waves<MODE>()))) void half_cols_kernel(const HalfSpecArgs a,
                                                              const double2* __restrict__ src,
                                                              double2* __restrict__ dst, int arr0,
                                                              int nb) {
