@@ -40,7 +40,7 @@ extern "C" {
 #define CFDJ_K_DIVIDE 2   /* column pass (FFT + divide by the FD symbol, Common.jl:119-121, +
                              inverse FFT), the substructured y-solve, or the divide kernel */
 #define CFDJ_K_FFT_INV 3  /* inverse transforms: hand-written row c2r pass, or rocFFT Z2D */
-#define CFDJ_K_COMM 4     /* halo exchange + FFT transposes (multi-GPU only) */
+#define CFDJ_K_COMM 4     /* collectives and halo exchanges (multi-GPU only) */
 #define CFDJ_K_COUNT 5
 
 /* Poisson implementation (cfdj_vm_set_poisson / cfdj_fps_set_poisson). */
@@ -50,10 +50,11 @@ extern "C" {
                                  ny 1024..8192, power-of-two rank counts (on y-slabs:
                                  all-to-all transposes of the half spectrum) */
 #define CFDJ_POISSON_SCHUR 3  /* y-slabs only: hand-written row FFTs + substructured y-solve
-                                 (chunked tridiagonal interiors, P x P separator system; two all-gathers
-                                 of 64 B per x-mode instead of transposes); square
-                                 power-of-two grids, 512..4096 rows per rank.  AUTO on
-                                 y-slabs picks it where supported. */
+                                 (chunked tridiagonal interiors, P x P separator system; one
+                                 all-gather of 48 B per x-mode and three rows per rank instead
+                                 of transposes -- it also carries the stencil's halo rows);
+                                 square power-of-two grids up to 16384^2, 512..4096 rows per
+                                 rank.  AUTO on y-slabs picks it where supported. */
 
 /* Poisson symbol (cfdj_fps_set_symbol). */
 #define CFDJ_SYMBOL_FD 0       /* Common.jl:119-121 / fft_p.jl:37-39: aa + bb cos kx + cc cos ky */
