@@ -265,21 +265,49 @@ struct StageTw {
   static constexpr int NS = Plan<L, NV>::ns(S);
   Tw<L, R, NS> t[NV / R];
 };
+// The last stage of L = 2 * 16^k (R = 2, NS = L/2 = 8 T, eight butterflies per thread):
+// butterfly b's twiddle is W_L^(tid + b T) = W_L^tid * W_16^b -- ONE table value and constants
+// where eight loaded values would sit in registers from before the exchange to the butterflies
+// (L = 8192 rows: 142-154 registers, one 512-thread workgroup per CU).  CFDJ_LAZY_R2=0: loads.
+#ifndef CFDJ_LAZY_R2
+#define CFDJ_LAZY_R2 1
+#endif
+template <int L, int S, int NV>
+constexpr bool lazy_r2() {
+  return CFDJ_LAZY_R2 != 0 && NV == 16 && Plan<L, NV>::radix(S) == 2 &&
+         Plan<L, NV>::ns(S) * 2 == L && Plan<L, NV>::ns(S) == 8 * Plan<L, NV>::T;
+}
 template <int L, int S, class TW, int NV = 16>
 __device__ __forceinline__ StageTw<L, S, NV> stage_tw(int tid, const TW& tw) {
   using ST = StageTw<L, S, NV>;
   ST st;
+  if constexpr (lazy_r2<L, S, NV>()) {
+    st.t[0] = load_tw<L, ST::R, ST::NS, TW>(tid, tw);
+  } else {
 #pragma unroll
-  for (int b = 0; b < NV / ST::R; ++b)
-    st.t[b] = load_tw<L, ST::R, ST::NS, TW>(tid + b * Plan<L, NV>::T, tw);
+    for (int b = 0; b < NV / ST::R; ++b)
+      st.t[b] = load_tw<L, ST::R, ST::NS, TW>(tid + b * Plan<L, NV>::T, tw);
+  }
   return st;
+}
+template <int DIR, int B>
+__device__ __forceinline__ void lazy_r2_butterflies(double2* v, double2 w) {
+  if constexpr (B < 8) {
+    v[2 * B + 1] = tw16<B, DIR>(cmul(v[2 * B + 1], w));
+    dft2<DIR>(v[2 * B], v[2 * B + 1]);
+    lazy_r2_butterflies<DIR, B + 1>(v, w);
+  }
 }
 template <int L, int S, int DIR, int NV>
 __device__ __forceinline__ void stage_regs(double2 (&v)[NV], const StageTw<L, S, NV>& st) {
   constexpr int R = Plan<L, NV>::radix(S);
   constexpr int NS = Plan<L, NV>::ns(S);
+  if constexpr (lazy_r2<L, S, NV>()) {
+    lazy_r2_butterflies<DIR, 0>(v, DIR < 0 ? st.t[0].w1 : cconj(st.t[0].w1));
+  } else {
 #pragma unroll
-  for (int b = 0; b < NV / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);
+    for (int b = 0; b < NV / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);
+  }
 }
 template <int L, int S, int DIR, class TW, int NV>
 __device__ __forceinline__ void stage_regs(double2 (&v)[NV], int tid, const TW& tw) {

@@ -683,12 +683,13 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 #define CFDJ_ROWS_NP_XR_MIN 2
 #endif
 // Minimum wavefronts per SIMD the small-item row kernels are compiled for (1: no constraint).
-// Rows of 8192 complex points are 512-thread workgroups, two wavefronts per SIMD each, and
-// at their 142-154 registers only one fits a CU; the 128-register cap that admits a second
-// (CFDJ_ROWS_NP_WAVES_8192=4) spills 19-33 registers and measured 158-162 us per pass at
-// 16384 x 2048 against 147-148 without.
+// Rows of 8192 complex points are 512-thread workgroups, two wavefronts per SIMD each: a
+// second workgroup per CU needs the kernel within 128 registers.  With eight loaded twiddles
+// of the radix-2 last stage held across the exchange they wanted 142-154 and the cap spilled
+// 19-33 (158-162 us per pass at 16384 x 2048 against 147-148 uncapped); with that stage's
+// twiddles formed from one table value (fft_lds.hpp: lazy_r2) they fit without spills.
 #ifndef CFDJ_ROWS_NP_WAVES_8192
-#define CFDJ_ROWS_NP_WAVES_8192 1
+#define CFDJ_ROWS_NP_WAVES_8192 4
 #endif
 // Rows of 4096 complex points (256-thread workgroups, 35 KB of LDS: four per CU): the forward
 // kernel of the y-slab path wants 138 registers, three workgroups per CU; capped at 128 it
@@ -697,9 +698,14 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 #ifndef CFDJ_ROWS_NP_WAVES_4096
 #define CFDJ_ROWS_NP_WAVES_4096 4
 #endif
+// (rows of 512 complex points, eight per 256-thread workgroup: the inverse kernel is at 129)
+#ifndef CFDJ_ROWS_NP_WAVES_512
+#define CFDJ_ROWS_NP_WAVES_512 4
+#endif
 template <int L>
 constexpr int rows_np_waves() {
-  return L >= 8192 ? CFDJ_ROWS_NP_WAVES_8192 : L == 4096 ? CFDJ_ROWS_NP_WAVES_4096 : 1;
+  return L >= 8192 ? CFDJ_ROWS_NP_WAVES_8192 : L == 4096 ? CFDJ_ROWS_NP_WAVES_4096 :
+         L == 512 ? CFDJ_ROWS_NP_WAVES_512 : 1;
 }
 
 template <int L, bool TILE>
