@@ -34,6 +34,11 @@ namespace cfdj {
 
 namespace {
 
+// Longest transform the small-item (non-persistent) row kernels take.
+#ifndef CFDJ_DST_NP_MAXM2
+#define CFDJ_DST_NP_MAXM2 8192
+#endif
+
 // Row passes: RP row pairs (2 RP rows) per work item, one packed FFT of length M2 each.
 template <int M2>
 struct DstRowCfg {
@@ -349,7 +354,7 @@ __global__ __launch_bounds__(DstNpCfg<M2>::THREADS)
 #define CFDJ_DST_FWD_NP 1
 #endif
 template <int M2>
-constexpr bool dst_fwd_np() { return CFDJ_DST_FWD_NP != 0 && M2 <= 4096; }
+constexpr bool dst_fwd_np() { return CFDJ_DST_FWD_NP != 0 && M2 <= CFDJ_DST_NP_MAXM2; }
 
 template <int M2>
 __global__ __launch_bounds__(DstNpCfg<M2>::THREADS) void dst_rows_fwd_np_kernel(
@@ -822,7 +827,7 @@ int dst_rows_grid_t(int ny, int ncu) {
 #define CFDJ_DST_INV_NP 1
 #endif
 template <int M2>
-constexpr bool dst_inv_np() { return CFDJ_DST_INV_NP != 0 && M2 <= 4096; }
+constexpr bool dst_inv_np() { return CFDJ_DST_INV_NP != 0 && M2 <= CFDJ_DST_NP_MAXM2; }
 template <int M2>
 int dst_rows_inv_grid_t(int ny, int ncu) {
   if (dst_inv_np<M2>() && ny % DstNpCfg<M2>::ROWS == 0) return ny / DstNpCfg<M2>::ROWS;
@@ -887,7 +892,13 @@ int dst_half_passes(int nx, int ny) {
   const char* e = std::getenv("CFDJ_DST_HALF");
   if (e && e[0] == '0') return 0;
   if (e && e[0] == '1') return 7;
-  return (nx >= 4096 ? 1 | 4 : 0) | (ny >= 2048 ? 2 : 0);
+  if (e && e[0] == 'm') return std::atoi(e + 1) & 7;  // (A/B: a mask of passes)
+  // columns from 2048 points on; rows never: at nx = 4096 the small-item odd-extension kernels
+  // (8192-point transforms, two 512-thread workgroups per CU since the remainder stage's
+  // twiddles stopped costing 24-47 registers) take 100 / 98 us per pass of a 4096^2 solve
+  // against the half-length kernels' 105 / 108
+  (void)nx;
+  return ny >= 2048 ? 2 : 0;
 }
 
 int dst_rows_grid(int nx, int ny, int ncu, int half) {

@@ -265,23 +265,27 @@ struct StageTw {
   static constexpr int NS = Plan<L, NV>::ns(S);
   Tw<L, R, NS> t[NV / R];
 };
-// The last stage of L = 2 * 16^k (R = 2, NS = L/2 = 8 T, eight butterflies per thread):
-// butterfly b's twiddle is W_L^(tid + b T) = W_L^tid * W_16^b -- ONE table value and constants
-// where eight loaded values would sit in registers from before the exchange to the butterflies
-// (L = 8192 rows: 142-154 registers, one 512-thread workgroup per CU).  CFDJ_LAZY_R2=0: loads.
-#ifndef CFDJ_LAZY_R2
-#define CFDJ_LAZY_R2 1
+// The remainder stage (the last one; R = 2 or 4: 8 or 4 butterflies per thread): butterfly b's
+// base twiddle is W_L^(tid + b T) = W_L^tid * W_16^b (T = L / 16) -- ONE table value, its
+// powers shared by the butterflies, and compile-time 16th roots where 16 / R loaded values
+// would sit in registers from before the exchange to the butterflies (L = 8192 rows: 142-154
+// registers, one 512-thread workgroup per CU, against 120-128).  Not for R = 8 (L = 2048: two
+// butterflies, nothing to win, and the seven shared powers cost the row kernels 7 registers
+// and an occupancy step).  CFDJ_LAZY_LAST_MAXR=0: every butterfly's twiddles from the table.
+#ifndef CFDJ_LAZY_LAST_MAXR
+#define CFDJ_LAZY_LAST_MAXR 4
 #endif
 template <int L, int S, int NV>
-constexpr bool lazy_r2() {
-  return CFDJ_LAZY_R2 != 0 && NV == 16 && Plan<L, NV>::radix(S) == 2 &&
-         Plan<L, NV>::ns(S) * 2 == L && Plan<L, NV>::ns(S) == 8 * Plan<L, NV>::T;
+constexpr bool lazy_last() {
+  constexpr int R = Plan<L, NV>::radix(S);
+  return NV == 16 && R <= CFDJ_LAZY_LAST_MAXR && Plan<L, NV>::ns(S) > 1 &&
+         Plan<L, NV>::ns(S) * R == L;
 }
 template <int L, int S, class TW, int NV = 16>
 __device__ __forceinline__ StageTw<L, S, NV> stage_tw(int tid, const TW& tw) {
   using ST = StageTw<L, S, NV>;
   ST st;
-  if constexpr (lazy_r2<L, S, NV>()) {
+  if constexpr (lazy_last<L, S, NV>()) {
     st.t[0] = load_tw<L, ST::R, ST::NS, TW>(tid, tw);
   } else {
 #pragma unroll
@@ -290,20 +294,41 @@ __device__ __forceinline__ StageTw<L, S, NV> stage_tw(int tid, const TW& tw) {
   }
   return st;
 }
-template <int DIR, int B>
-__device__ __forceinline__ void lazy_r2_butterflies(double2* v, double2 w) {
-  if constexpr (B < 8) {
-    v[2 * B + 1] = tw16<B, DIR>(cmul(v[2 * B + 1], w));
-    dft2<DIR>(v[2 * B], v[2 * B + 1]);
-    lazy_r2_butterflies<DIR, B + 1>(v, w);
+// input r of butterfly B times base^r (pw[r], shared by the butterflies) times W_16^(r B)
+template <int R, int DIR, int B, int Rr>
+__device__ __forceinline__ void lazy_last_twiddle(double2* v, const double2* pw) {
+  if constexpr (Rr < R) {
+    v[B * R + Rr] = tw16<Rr * B, DIR>(cmul(v[B * R + Rr], pw[Rr]));
+    lazy_last_twiddle<R, DIR, B, Rr + 1>(v, pw);
+  }
+}
+template <int R, int DIR, int B>
+__device__ __forceinline__ void lazy_last_butterflies(double2* v, const double2* pw) {
+  if constexpr (B < 16 / R) {
+    lazy_last_twiddle<R, DIR, B, 1>(v, pw);
+    dft<R, DIR>(&v[B * R]);
+    lazy_last_butterflies<R, DIR, B + 1>(v, pw);
   }
 }
 template <int L, int S, int DIR, int NV>
 __device__ __forceinline__ void stage_regs(double2 (&v)[NV], const StageTw<L, S, NV>& st) {
   constexpr int R = Plan<L, NV>::radix(S);
   constexpr int NS = Plan<L, NV>::ns(S);
-  if constexpr (lazy_r2<L, S, NV>()) {
-    lazy_r2_butterflies<DIR, 0>(v, DIR < 0 ? st.t[0].w1 : cconj(st.t[0].w1));
+  if constexpr (lazy_last<L, S, NV>()) {
+    // the powers of the base twiddle W_L^tid, in the transform's direction
+    double2 pw[R];
+    pw[1] = DIR < 0 ? st.t[0].w1 : cconj(st.t[0].w1);
+    if constexpr (R >= 4) {
+      pw[2] = cmul(pw[1], pw[1]);
+      pw[3] = cmul(pw[2], pw[1]);
+    }
+    if constexpr (R >= 8) {
+      pw[4] = DIR < 0 ? st.t[0].w4 : cconj(st.t[0].w4);
+      pw[5] = cmul(pw[4], pw[1]);
+      pw[6] = cmul(pw[4], pw[2]);
+      pw[7] = cmul(pw[4], pw[3]);
+    }
+    lazy_last_butterflies<R, DIR, 0>(v, pw);
   } else {
 #pragma unroll
     for (int b = 0; b < NV / R; ++b) butterfly<L, R, NS, DIR>(&v[b * R], st.t[b]);

@@ -687,7 +687,7 @@ __global__ __launch_bounds__((RowCfg<L, false>::THREADS)) void rows_inv_kernel(
 // second workgroup per CU needs the kernel within 128 registers.  With eight loaded twiddles
 // of the radix-2 last stage held across the exchange they wanted 142-154 and the cap spilled
 // 19-33 (158-162 us per pass at 16384 x 2048 against 147-148 uncapped); with that stage's
-// twiddles formed from one table value (fft_lds.hpp: lazy_r2) they fit without spills.
+// twiddles formed from one table value (fft_lds.hpp: lazy_last) they fit without spills.
 #ifndef CFDJ_ROWS_NP_WAVES_8192
 #define CFDJ_ROWS_NP_WAVES_8192 4
 #endif

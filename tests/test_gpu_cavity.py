@@ -302,7 +302,7 @@ def test_gpu_cavity_rhs_call_leaves_the_state_alone(lib):
 
 
 @pytest.mark.parametrize("half", ["0", "1"])
-@pytest.mark.parametrize("n", [512, 2048])
+@pytest.mark.parametrize("n", [512, 2048, 4096])
 def test_gpu_fps_sine_both_transform_routes(lib, monkeypatch, n, half):
     """lid_driven_cavity.jl:11-21 by both routes to FFTW's RODFT00: the odd extension of a row
     pair (a complex FFT of 2n points; CFDJ_DST_HALF=0) and the half-length transform (n points,
