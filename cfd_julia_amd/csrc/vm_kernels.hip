@@ -334,42 +334,41 @@ __global__ __launch_bounds__(64 * kTallW) CFDJ_TALL_ATTR void vm_stage_tall_kern
     halo = r[xh];
   }
   const StageCoef k = p.k;
-  Win ww[NR], sw[NR];
-#pragma unroll
-  for (int j = 0; j < NR; ++j) {
-    ww[j].a = wv[j].x;
-    ww[j].b = wv[j].y;
-    sw[j].a = sv[j].x;
-    sw[j].b = sv[j].y;
-    ww[j].l = __shfl_up(wv[j].y, 1, kWave);
-    ww[j].r = __shfl_down(wv[j].x, 1, kWave);
-    sw[j].l = __shfl_up(sv[j].y, 1, kWave);
-    sw[j].r = __shfl_down(sv[j].x, 1, kWave);
-    const double lw = __shfl(halo, 2 * j, kWave), ls = __shfl(halo, 2 * j + 1, kWave);
-    const double rw = __shfl(halo, 2 * NR + 2 * j, kWave);
-    const double rs = __shfl(halo, 2 * NR + 2 * j + 1, kWave);
-    if (lane == 0) {
-      ww[j].l = lw;
-      sw[j].l = ls;
-    }
-    if (lane == kWave - 1) {
-      ww[j].r = rw;
-      sw[j].r = rs;
-    }
-  }
+  // a row's window (its two x-neighbours from the neighbouring lanes, the wave's edge columns
+  // from the halo load), formed when the row first enters a stencil: three windows per field
+  // are live, not NR
+  auto window = [&](const double2& c, int jh, int field) {
+    Win w;
+    w.a = c.x;
+    w.b = c.y;
+    w.l = __shfl_up(c.y, 1, kWave);
+    w.r = __shfl_down(c.x, 1, kWave);
+    const double hl = __shfl(halo, 2 * jh + field, kWave);
+    const double hr = __shfl(halo, 2 * NR + 2 * jh + field, kWave);
+    if (lane == 0) w.l = hl;
+    if (lane == kWave - 1) w.r = hr;
+    return w;
+  };
+  Win wm = window(wv[0], 0, 0), sm = window(sv[0], 0, 1);
+  Win wc = window(wv[1], 1, 0), sc = window(sv[1], 1, 1);
 #pragma unroll
   for (int j = 0; j < G; ++j) {
+    const Win wp = window(wv[j + 2], j + 2, 0), sp = window(sv[j + 2], j + 2, 1);
     double r0, r1;
-    pair_rhs(ww[j], ww[j + 1], ww[j + 2], sw[j], sw[j + 1], sw[j + 2], k, r0, r1);
+    pair_rhs(wm, wc, wp, sm, sc, sp, k, r0, r1);
     double2 o;
-    o.x = stage_update<STAGE>(r0, ww[j + 1].a, wnv[j].x, k);
-    o.y = stage_update<STAGE>(r1, ww[j + 1].b, wnv[j].y, k);
+    o.x = stage_update<STAGE>(r0, wc.a, wnv[j].x, k);
+    o.y = stage_update<STAGE>(r1, wc.b, wnv[j].y, k);
 #ifdef CFDJ_TALL_PLAIN_STORE
     *reinterpret_cast<double2*>(p.out + (size_t)(y0 + j) * nx + x) = o;
 #else
     store_stream<NT>(reinterpret_cast<double2*>(p.out + (size_t)(y0 + j) * nx + x), o);
 #endif
     outs[wave * G + j][lane] = o;
+    wm = wc;
+    sm = sc;
+    wc = wp;
+    sc = sp;
   }
   __syncthreads();
   if (wave == 0) {
